@@ -1,0 +1,322 @@
+"""Generate the committed golden vectors under ``tests/golden/`` (run HERE, in
+the container that has /root/reference and torch's fbgemm engine):
+
+    python oracle/make_golden.py
+
+What pins what:
+  * per-op vectors come from torch.ao / FBGEMM (torch 2.10.0+rocm7.0 wheel,
+    engine ``fbgemm``) on seeded random data, and are re-checked against the
+    numpy restatement ``oracle/qref.py`` here (assertions below) and in
+    ``tests/test_oracle_golden.py``;
+  * the whole-net vectors come from the torch.ao eager static-int8 build of the
+    restated SimpleConvNet (``oracle/torch_ref.py``); the restatement itself is
+    checked against the reference's own ``models.baseline_model.SimpleConvNet``
+    and ``models.static_ptq_model.StaticPTQModel`` imported from /root/reference
+    (same state_dict -> identical outputs), so the fixtures are pinned to the
+    reference's code, not only to our reading of it.
+
+The reference source never leaves /root/reference: only numbers are written.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.ao.nn.quantized as nnq
+import torch.ao.nn.intrinsic.quantized as nniq
+import torch.ao.nn.quantized.dynamic as nnqd
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+from oracle import qref, torch_ref as tr  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+F32 = np.float32
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def qt(arr, scale, zp, dtype=torch.quint8):
+    return torch._make_per_tensor_quantized_tensor(torch.from_numpy(arr), float(scale), int(zp)) \
+        if dtype == torch.quint8 else torch._make_per_tensor_quantized_tensor(
+            torch.from_numpy(arr), float(scale), int(zp))
+
+
+# ----------------------------------------------------------------- per-op
+def gen_quantize(rng):
+    cases = {}
+    for i, (scale, zp) in enumerate([(0.0203, 120), (0.5, 11), (1.0, 127), (0.013, 0), (2.0 ** -7, 3)]):
+        x = (rng.standard_normal(4096) * 2).astype(F32)
+        # exact ties and clamping extremes
+        ties = (np.arange(-40, 40) + 0.5).astype(F32) * F32(scale)
+        x = np.concatenate([x, ties, np.array([1e9, -1e9, 0.0, -0.0], F32)]).astype(F32)
+        q = torch.quantize_per_tensor(torch.from_numpy(x), float(scale), zp, torch.quint8).int_repr().numpy()
+        assert (q == qref.quantize_per_tensor(x, scale, zp)).all(), f"quantize case {i}"
+        dq = torch.quantize_per_tensor(torch.from_numpy(x), float(scale), zp, torch.quint8).dequantize().numpy()
+        assert (dq == qref.dequantize(q, scale, zp)).all()
+        cases[f"q{i}_x"] = x
+        cases[f"q{i}_scale"] = F32(scale)
+        cases[f"q{i}_zp"] = np.int64(zp)
+        cases[f"q{i}_q"] = q
+        cases[f"q{i}_dq"] = dq
+    np.savez_compressed(os.path.join(OUT, "ops_quantize.npz"), **cases)
+
+
+def gen_qparams(rng):
+    import torch.ao.quantization as tq
+    mins, maxs, aff_s, aff_z, sym_s = [], [], [], [], []
+    for _ in range(400):
+        lo = F32(-abs(rng.standard_normal()) * rng.choice([0, 0.01, 1, 10]))
+        hi = F32(abs(rng.standard_normal()) * rng.choice([0, 0.01, 1, 10]))
+        ob = tq.MinMaxObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine)
+        ob(torch.tensor([lo, hi]))
+        s, z = ob.calculate_qparams()
+        sym = tq.MinMaxObserver(dtype=torch.qint8, qscheme=torch.per_tensor_symmetric)
+        sym(torch.tensor([lo, hi]))
+        ss, _ = sym.calculate_qparams()
+        ms, mz = qref.qparams_affine(lo, hi)
+        assert ms == F32(s.item()) and mz == int(z.item()), (lo, hi)
+        assert qref.qparams_symmetric(lo, hi)[0] == F32(ss.item())
+        mins.append(lo), maxs.append(hi), aff_s.append(s.item()), aff_z.append(z.item()), sym_s.append(ss.item())
+    np.savez_compressed(os.path.join(OUT, "ops_qparams.npz"), min=np.array(mins, F32), max=np.array(maxs, F32),
+                        aff_scale=np.array(aff_s, F32), aff_zp=np.array(aff_z, np.int64),
+                        sym_scale=np.array(sym_s, F32))
+
+
+def _conv_case(rng, n, h, cin, cout, zx, relu, per_channel, zy):
+    s_x = F32(rng.uniform(0.01, 0.03))
+    qx = rng.integers(0, 256, (n, h, h, cin)).astype(np.uint8)
+    w = (rng.standard_normal((cout, cin, 3, 3)) * 0.05).astype(F32)
+    b = (rng.standard_normal(cout) * 0.5).astype(F32)
+    if per_channel:
+        s_w, _ = qref.qparams_symmetric(w.reshape(cout, -1).min(1), w.reshape(cout, -1).max(1))
+        wq = torch.quantize_per_channel(torch.from_numpy(w), torch.from_numpy(s_w.astype(np.float64)),
+                                        torch.zeros(cout, dtype=torch.long), 0, torch.qint8)
+    else:
+        s_w, _ = qref.qparams_symmetric(w.min(), w.max())
+        wq = torch.quantize_per_tensor(torch.from_numpy(w), float(s_w), 0, torch.qint8)
+    wi = wq.int_repr().numpy()
+    assert (qref.quantize_weight(w, s_w) == wi).all()
+    s_y = F32(rng.uniform(0.01, 0.05))
+    mod = (nniq.ConvReLU2d if relu else nnq.Conv2d)(cin, cout, 3, padding=1)
+    mod.set_weight_bias(wq, torch.from_numpy(b))
+    mod.scale, mod.zero_point = float(s_y), int(zy)
+    xin = torch._make_per_tensor_quantized_tensor(torch.from_numpy(np.ascontiguousarray(qx.transpose(0, 3, 1, 2))),
+                                                  float(s_x), int(zx))
+    out = mod(xin).int_repr().permute(0, 2, 3, 1).contiguous().numpy()
+    w_ohwi = np.ascontiguousarray(wi.transpose(0, 2, 3, 1))
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    mine = qref.conv3x3_q(qx, zx, w_ohwi, u, v, mult, zy, relu)
+    assert (mine == out).all(), f"conv case mismatch {(mine != out).sum()}"
+    return dict(qx=qx, zx=np.int64(zx), s_x=s_x, w=w_ohwi, s_w=np.asarray(s_w, F32), b=b, s_y=s_y,
+                zy=np.int64(zy), relu=np.int64(relu), out=out)
+
+
+def gen_conv(rng):
+    cases = {}
+    specs = [  # n, h, cin, cout, zx, relu, per_channel, zy
+        (2, 8, 3, 64, 120, True, False, 0),
+        (2, 8, 64, 64, 0, True, False, 0),
+        (2, 8, 64, 128, 0, False, False, 77),
+        (1, 8, 128, 256, 5, True, True, 0),
+        (2, 4, 256, 256, 0, True, False, 0),
+        (2, 16, 64, 64, 9, False, True, 130),
+    ]
+    for i, sp in enumerate(specs):
+        for k, v in _conv_case(rng, *sp).items():
+            cases[f"c{i}_{k}"] = v
+    cases["n"] = np.int64(len(specs))
+    np.savez_compressed(os.path.join(OUT, "ops_conv.npz"), **cases)
+
+
+def gen_linear(rng):
+    cases = {}
+    specs = [(16, 1024, 256, 0, True), (16, 512, 10, 0, False), (8, 64, 32, 37, False)]
+    for i, (m, k, n, zx, relu) in enumerate(specs):
+        s_x = F32(rng.uniform(0.01, 0.03))
+        qx = rng.integers(0, 256, (m, k)).astype(np.uint8)
+        w = (rng.standard_normal((n, k)) * 0.03).astype(F32)
+        b = (rng.standard_normal(n) * 0.5).astype(F32)
+        s_w, _ = qref.qparams_symmetric(w.min(), w.max())
+        wq = torch.quantize_per_tensor(torch.from_numpy(w), float(s_w), 0, torch.qint8)
+        s_y, zy = F32(rng.uniform(0.05, 0.5)), int(rng.integers(0, 200))
+        if relu:
+            zy = 0
+        mod = (nniq.LinearReLU if relu else nnq.Linear)(k, n)
+        mod.set_weight_bias(wq, torch.from_numpy(b))
+        mod.scale, mod.zero_point = float(s_y), zy
+        out = mod(torch._make_per_tensor_quantized_tensor(torch.from_numpy(qx), float(s_x), zx)).int_repr().numpy()
+        u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+        mine = qref.linear_q(qx, zx, wq.int_repr().numpy(), u, v, mult, zy, relu)
+        assert (mine == out).all(), f"linear case {i}: {(mine != out).sum()}"
+        cases.update({f"l{i}_qx": qx, f"l{i}_zx": np.int64(zx), f"l{i}_s_x": s_x, f"l{i}_w": wq.int_repr().numpy(),
+                      f"l{i}_s_w": F32(s_w), f"l{i}_b": b, f"l{i}_s_y": s_y, f"l{i}_zy": np.int64(zy),
+                      f"l{i}_relu": np.int64(relu), f"l{i}_out": out})
+    cases["n"] = np.int64(len(specs))
+    np.savez_compressed(os.path.join(OUT, "ops_linear.npz"), **cases)
+
+
+def gen_dynamic_linear(rng):
+    torch.backends.quantized.engine = "fbgemm"
+    cases = {}
+    specs = [(32, 1024, 256), (32, 512, 10), (7, 256, 33)]
+    for i, (m, k, n) in enumerate(specs):
+        lin = torch.nn.Linear(k, n)
+        with torch.no_grad():
+            lin.weight.copy_(torch.from_numpy((rng.standard_normal((n, k)) * 0.03).astype(F32)))
+            lin.bias.copy_(torch.from_numpy((rng.standard_normal(n) * 0.3).astype(F32)))
+        dq = torch.ao.quantization.quantize_dynamic(
+            torch.nn.Sequential(lin), {torch.nn.Linear}, dtype=torch.qint8)[0]
+        x = (rng.standard_normal((m, k)) * rng.uniform(0.5, 3)).astype(F32)
+        y = dq(torch.from_numpy(x)).detach().numpy()
+        wq = dq.weight()
+        mine = qref.linear_dynamic(x, wq.int_repr().numpy(), F32(wq.q_scale()), dq.bias().detach().numpy())
+        assert (mine == y).all(), f"dynamic linear case {i}: {(mine != y).sum()} / {y.size}"
+        cases.update({f"d{i}_x": x, f"d{i}_w": wq.int_repr().numpy(), f"d{i}_s_w": F32(wq.q_scale()),
+                      f"d{i}_b": dq.bias().detach().numpy().astype(F32), f"d{i}_y": y})
+    cases["n"] = np.int64(len(specs))
+    np.savez_compressed(os.path.join(OUT, "ops_dynamic_linear.npz"), **cases)
+
+
+# ----------------------------------------------------------------- whole net
+def extract_qmodel(q, per_channel=False):
+    """Pull the quantized parameters out of the torch.ao static-int8 model into
+    the oracle's dict form (qref.static_int8_forward)."""
+    qm = {"in_scale": F32(q.quant.scale.item()), "in_zp": int(q.quant.zero_point.item())}
+    s_x = qm["in_scale"]
+    for name in [f"conv{i}" for i in range(1, 7)] + ["fc1", "fc2"]:
+        m = getattr(q, name)
+        w = m.weight()
+        wi = w.int_repr().numpy()
+        if name.startswith("conv"):
+            wi = np.ascontiguousarray(wi.transpose(0, 2, 3, 1))
+        if w.qscheme() == torch.per_tensor_symmetric or w.qscheme() == torch.per_tensor_affine:
+            s_w = F32(w.q_scale())
+        else:
+            s_w = w.q_per_channel_scales().numpy().astype(F32)
+        b = m.bias().detach().numpy().astype(F32)
+        s_y, z_y = F32(m.scale), int(m.zero_point)
+        u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+        if name == "fc1":
+            wi = np.ascontiguousarray(wi[:, qref.flatten_perm_nhwc_to_nchw()])
+        qm.update({name + "_w": wi, name + "_u": u, name + "_v": v, name + "_mult": mult,
+                   name + "_zp": z_y, name + "_scale": s_y, name + "_s_w": np.asarray(s_w, F32),
+                   name + "_b": b})
+        s_x = s_y
+    return qm
+
+
+def check_restatement_against_reference(sd):
+    """Import the reference models (read-only, here only) and check that our
+    restated topology and our StaticPTQModel counterpart agree bit-for-bit."""
+    sys.path.insert(0, "/root/reference")
+    try:
+        from models.baseline_model import SimpleConvNet
+        from models.static_ptq_model import StaticPTQModel
+    finally:
+        sys.path.pop(0)
+    x = torch.from_numpy(tr.synthetic_images(16, 5))
+    ref = SimpleConvNet()
+    ref.load_state_dict(sd)
+    ref.eval()
+    mine = tr.SimpleConvNetRef()
+    mine.load_state_dict(sd)
+    mine.eval()
+    with torch.no_grad():
+        assert torch.equal(ref(x), mine(x)), "SimpleConvNet restatement differs"
+        sp = StaticPTQModel()
+        sp.fp32_model.load_state_dict(sd)
+        ref_q = sp.quantize()
+        my_q = tr.build_static_ptq_cpu(mine)
+        assert torch.equal(ref_q(x), my_q(x)), "StaticPTQModel counterpart differs"
+    return True
+
+
+def gen_net(per_channel=False, batch=64):
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    calib = tr.synthetic_images(512, 1)
+    fp = tr.reference_fp32_model(0, calib)
+    sd = fp.state_dict()
+    check_restatement_against_reference(sd)
+    q = tr.build_static_int8_cpu(fp, [torch.from_numpy(calib)], per_channel=per_channel)
+    qm = extract_qmodel(q, per_channel)
+    x = tr.synthetic_images(batch, 0)
+    with torch.no_grad():
+        ref = q(torch.from_numpy(x)).numpy()
+    logits, ql, inter = qref.static_int8_forward(x, qm, keep=True)
+    assert (logits == ref).all(), "oracle != torch.ao static int8"
+    # torch.ao intermediates (NHWC u8) for the per-layer hashes
+    outs = {}
+    hooks = [getattr(q, f"conv{i}").register_forward_hook(
+        lambda m, a, o, k=i: outs.__setitem__(k, o)) for i in range(1, 7)]
+    with torch.no_grad():
+        q(torch.from_numpy(x))
+    for h in hooks:
+        h.remove()
+    rec = {"batch": np.int64(batch), "x_sha": sha(x), "logits": ref, "q_logits": ql,
+           "argmax": qref.argmax_rows(ref), "per_channel": np.int64(per_channel)}
+    for i in range(1, 7):
+        o = outs[i].int_repr().permute(0, 2, 3, 1).contiguous().numpy()
+        if i % 2 == 0:
+            o = qref.maxpool2x2_nhwc(o)
+        assert (o == inter[f"conv{i}"]).all()
+        rec[f"conv{i}_sha"] = sha(o)
+        rec[f"conv{i}_slice"] = o[:2, :2, :2, :].copy()
+    rec["fc1_sha"] = sha(inter["fc1"])
+    # BN statistics after recalibration (the only non-regenerable fp32 state)
+    for i in range(1, 8):
+        rec[f"bn{i}_mean"] = sd[f"bn{i}.running_mean"].numpy()
+        rec[f"bn{i}_var"] = sd[f"bn{i}.running_var"].numpy()
+    # quantized parameters: scales/zps in full, int8 weights by hash
+    for k, v in qm.items():
+        if k.endswith("_w"):
+            rec[k + "_sha"] = sha(v)
+        else:
+            rec["qm_" + k] = np.asarray(v)
+    # CPU reference paths on the same batch (top-1 parity anchors)
+    with torch.no_grad():
+        xt = torch.from_numpy(x)
+        rec["fp32_logits"] = fp(xt).numpy()
+        rec["static_ptq_logits"] = tr.build_static_ptq_cpu(fp)(xt).numpy()
+        rec["dynamic_ptq_logits"] = tr.build_dynamic_ptq_cpu(fp)(xt).numpy()
+        qdq = tr.build_qdq_cpu(fp, [torch.from_numpy(calib)], per_channel=per_channel)
+        rec["qdq_logits"] = qdq(xt).numpy()
+        for i in range(1, 7):
+            c = getattr(qdq, f"conv{i}")
+            rec[f"qdq_conv{i}_in_scale"] = F32(c.quant.scale.item())
+            rec[f"qdq_conv{i}_in_zp"] = np.int64(c.quant.zero_point.item())
+            rec[f"qdq_conv{i}_out_scale"] = F32(c.op.scale)
+            rec[f"qdq_conv{i}_out_zp"] = np.int64(c.op.zero_point)
+        rec["qdq_fc1_in_scale"] = F32(qdq.fc1.quant.scale.item())
+        rec["qdq_fc1_in_zp"] = np.int64(qdq.fc1.quant.zero_point.item())
+        rec["qdq_fc1_out_scale"] = F32(qdq.fc1.op.scale)
+        rec["qdq_fc1_out_zp"] = np.int64(qdq.fc1.op.zero_point)
+    name = "net_static_int8_pc.npz" if per_channel else "net_static_int8.npz"
+    np.savez_compressed(os.path.join(OUT, name), **rec)
+    return rec
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.backends.quantized.engine = "fbgemm"
+    rng = np.random.Generator(np.random.PCG64(1234))
+    gen_quantize(rng)
+    gen_qparams(rng)
+    gen_conv(rng)
+    gen_linear(rng)
+    gen_dynamic_linear(rng)
+    gen_net(per_channel=False)
+    gen_net(per_channel=True)
+    for f in sorted(os.listdir(OUT)):
+        print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()
