@@ -1,0 +1,54 @@
+// Shared device helpers for the gfx950 int8 ConvNet kernels.
+//
+// Numerics follow FBGEMM's vector epilogue exactly (see oracle/qref.py for the
+// CPU restatement and the torch-wheel disassembly it was read from):
+//   t  = fmaf(u_k, v_k, fp32(acc))          (per-tensor: u=b, v=fp32(1/aws);
+//                                            per-channel: u=fp32(b/aws), v=1)
+//   ab = fp32(t * mult_k)
+//   y  = clamp(rne(ab) + zp, relu ? zp : 0, 255)
+// Every kernel is compiled with -ffp-contract=off so that no other
+// multiply/add pair is fused behind our back.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+#define QCN_DEV __device__ __forceinline__
+
+QCN_DEV int requant_one(int acc, float u, float v, float mult, int zp, int lo) {
+  float a = (float)acc;                      // v_cvt_f32_i32: RNE, like cvtdq2ps
+  float t = __builtin_fmaf(u, v, a);
+  float ab = t * mult;
+  ab = __builtin_rintf(ab);                  // v_rndne_f32: ties to even
+  ab = fminf(fmaxf(ab, -65536.0f), 65536.0f);  // keep the int conversion defined
+  int r = (int)ab + zp;
+  r = r < lo ? lo : r;
+  r = r > 255 ? 255 : r;
+  return r;
+}
+
+// Per-layer QDQ second stage (reference CustomQuantizedConv2d chain,
+// custom_quantization_model.py:41-45 + F.relu at :237-250): the u8 output q of
+// this layer (scale s1, zero point z1) is dequantized, ReLU'd, and quantized
+// with the NEXT layer's input qparams (inv = fp32(1/s2), z2), in the same fp32
+// op order as aten dequantize / quantize_per_tensor (oracle qref A1/A7).
+QCN_DEV int qdq_next(int q, float s1, int z1, float inv2, int z2) {
+  float x = (float)(q - z1) * s1;
+  x = x > 0.0f ? x : 0.0f;
+  float t = x * inv2;
+  t = fminf(t, 1.0e9f);
+  t = __builtin_rintf(t);
+  int r = (int)t + z2;
+  r = r < 0 ? 0 : r;
+  r = r > 255 ? 255 : r;
+  return r;
+}
+
+QCN_DEV uint32_t xor80(uint32_t v) { return v ^ 0x80808080u; }
+
+QCN_DEV uint32_t splat_u8(int b) {
+  uint32_t x = (uint32_t)(b & 0xff);
+  return x | (x << 8) | (x << 16) | (x << 24);
+}

@@ -1,0 +1,194 @@
+"""Tensor-level wrappers over the C ABI (torch tensors are plumbing: device
+memory + the current HIP stream).  Every op launches on
+``torch.cuda.current_stream()`` and never synchronizes, so sequences of them
+can be captured in a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import QDQ, check
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _need(t, dtype, name):
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+
+
+def lib():
+    return _lib.load()
+
+
+# ----------------------------------------------------------------- A1 / A7
+def quantize(x, scale, zero_point, nhwc=True, out=None):
+    """fp32 NCHW -> u8 (NHWC if nhwc) with aten quantize_per_tensor numerics."""
+    _need(x, torch.float32, "quantize.x")
+    n, c, h, w = x.shape
+    if out is None:
+        shape = (n, h, w, c) if nhwc else (n, c, h, w)
+        out = torch.empty(shape, dtype=torch.uint8, device=x.device)
+    check(lib().qcn_quantize_f32_u8(_ptr(x), _ptr(out), n, c, h, w, int(bool(nhwc)),
+                                    float(scale), int(zero_point), _stream()), "quantize")
+    return out
+
+
+def dequantize(q, scale, zero_point, out=None):
+    _need(q, torch.uint8, "dequantize.q")
+    if out is None:
+        out = torch.empty(q.shape, dtype=torch.float32, device=q.device)
+    check(lib().qcn_dequantize_u8_f32(_ptr(q), _ptr(out), q.numel(), float(scale),
+                                      int(zero_point), _stream()), "dequantize")
+    return out
+
+
+# ---------------------------------------------------------------------- A2
+class MinMaxObserver:
+    """Device-side running min/max (MinMaxObserver.forward semantics)."""
+
+    def __init__(self, device="cuda"):
+        self.state = torch.empty(2, dtype=torch.float32, device=device)
+        self.reset()
+
+    def reset(self):
+        check(lib().qcn_minmax_reset(_ptr(self.state), _stream()), "minmax_reset")
+
+    def __call__(self, x):
+        _need(x, torch.float32, "minmax.x")
+        check(lib().qcn_minmax_f32(_ptr(x), x.numel(), _ptr(self.state), _stream()), "minmax")
+        return x
+
+    def values(self):
+        v = self.state.cpu().numpy()
+        return np.float32(v[0]), np.float32(v[1])
+
+
+# --------------------------------------------------------------- A10 / A11
+def maxpool2x2(x):
+    _need(x, torch.uint8, "maxpool.x")
+    n, h, w, c = x.shape
+    out = torch.empty((n, h // 2, w // 2, c), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_maxpool2x2_u8_nhwc(_ptr(x), n, h, w, c, _ptr(out), _stream()), "maxpool")
+    return out
+
+
+def argmax(x):
+    _need(x, torch.float32, "argmax.x")
+    rows, cols = x.shape
+    out = torch.empty(rows, dtype=torch.int64, device=x.device)
+    check(lib().qcn_argmax_f32(_ptr(x), rows, cols, _ptr(out), _stream()), "argmax")
+    return out
+
+
+# ------------------------------------------------------------------- packing
+def pack_conv3x3(w_oihw: np.ndarray):
+    """Host packing of s8 OIHW weights -> (packed bytes, wsum int32)."""
+    w = np.ascontiguousarray(w_oihw, dtype=np.int8)
+    cout, cin = w.shape[:2]
+    out = np.empty(lib().qcn_conv3x3_packed_size(cin, cout), np.int8)
+    wsum = np.empty(cout, np.int32)
+    check(lib().qcn_pack_conv3x3_weight(w.ctypes.data, cout, cin, out.ctypes.data,
+                                        wsum.ctypes.data), "pack_conv3x3")
+    return out, wsum
+
+
+def pack_conv1(w_oihw: np.ndarray):
+    w = np.ascontiguousarray(w_oihw, dtype=np.int8)
+    out = np.empty(64 * 32, np.int8)
+    wsum = np.empty(64, np.int32)
+    check(lib().qcn_pack_conv1_weight(w.ctypes.data, w.shape[0], out.ctypes.data,
+                                      wsum.ctypes.data), "pack_conv1")
+    return out, wsum
+
+
+def qdq_struct(s1, z1, s2, z2):
+    return QDQ(np.float32(s1), int(z1), np.float32(np.float32(1.0) / np.float32(s2)), int(z2))
+
+
+# ------------------------------------------------------------- A5/A6 + A9
+def conv3x3(x, x_zp, w_packed, cout, u, v, mult, corr, y_zp, relu, pool, qdq=None, out=None):
+    _need(x, torch.uint8, "conv.x")
+    n, h, w, cin = x.shape
+    oh, ow = (h // 2, w // 2) if pool else (h, w)
+    if out is None:
+        out = torch.empty((n, oh, ow, cout), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_conv3x3_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(w_packed), cout,
+                                      _ptr(u), _ptr(v), _ptr(mult), _ptr(corr), int(y_zp),
+                                      int(bool(relu)), int(bool(pool)),
+                                      C.byref(qdq) if qdq is not None else None, _ptr(out),
+                                      _stream()), "conv3x3")
+    return out
+
+
+def conv1_f32(x, in_scale, in_zp, w1_packed, u, v, mult, corr, y_zp, relu, qdq=None, out=None,
+              q_in=None):
+    _need(x, torch.float32, "conv1.x")
+    n, c, h, w = x.shape
+    if c != 3 or h != w:
+        raise ValueError("conv1_f32 expects [n,3,hw,hw]")
+    if out is None:
+        out = torch.empty((n, h, w, 64), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_conv1_f32_nchw(_ptr(x), n, h, float(in_scale), int(in_zp), _ptr(w1_packed),
+                                   _ptr(u), _ptr(v), _ptr(mult), _ptr(corr), int(y_zp),
+                                   int(bool(relu)), C.byref(qdq) if qdq is not None else None,
+                                   _ptr(out), _ptr(q_in), _stream()), "conv1")
+    return out
+
+
+def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=False, out=None,
+              out_f=None):
+    _need(x, torch.uint8, "linear.x")
+    m, k = x.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.uint8, device=x.device)
+    if want_fp32 and out_f is None:
+        out_f = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    check(lib().qcn_linear_u8s8(_ptr(x), m, k, int(x_zp), _ptr(w), n, _ptr(u), _ptr(v), _ptr(mult),
+                                _ptr(corr), int(y_zp), int(bool(relu)), _ptr(out),
+                                _ptr(out_f) if want_fp32 else None, float(y_scale), _stream()),
+          "linear_u8s8")
+    return (out, out_f) if want_fp32 else out
+
+
+def linear_dynamic(x, w, w_scale, wsum, bias, reduce_range=True, workspace=None, out=None):
+    """quantized::linear_dynamic on the device (fp32 in, fp32 out)."""
+    _need(x, torch.float32, "linear_dynamic.x")
+    m, k = x.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    need = lib().qcn_linear_dynamic_workspace_size(m, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    per_channel = int(w_scale.numel() > 1)
+    check(lib().qcn_linear_dynamic_f32(_ptr(x), m, k, _ptr(w), n, _ptr(w_scale), per_channel,
+                                       _ptr(wsum), _ptr(bias), int(bool(reduce_range)), _ptr(out),
+                                       _ptr(workspace), _stream()), "linear_dynamic")
+    return out
+
+
+def linear_f32(x, w, b, relu_in=False, out=None):
+    _need(x, torch.float32, "linear_f32.x")
+    m, k = x.shape
+    n = w.shape[0]
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    check(lib().qcn_linear_f32(_ptr(x), m, k, _ptr(w), n, _ptr(b), int(bool(relu_in)), _ptr(out),
+                               _stream()), "linear_f32")
+    return out

@@ -1,0 +1,380 @@
+"""The int8 SimpleConvNet executor on MI355X.
+
+``QuantizedConvNet`` holds the quantized model in HBM (packed s8 weights,
+per-channel fp32 epilogue constants, int32 zero-point corrections) and runs the
+forward as a fixed sequence of hand-written HIP kernels on the current stream:
+
+  static (full int8, BASELINE config 3):
+    conv1_f32 (quantize + conv1 + ReLU)  -> conv2(+pool) -> conv3 -> conv4(+pool)
+    -> conv5 -> conv6(+pool) -> fc1(+ReLU) -> fc2 (+ DeQuantStub, fp32 logits)
+  qdq (per-layer QDQ, BASELINE config 2 — custom_quantization_model.py:202-261
+       with its stubs live):
+    every conv requantizes to its own output qparams, then the epilogue does
+    dequantize -> ReLU -> quantize(next layer's input qparams); fc1 likewise,
+    then the fp32 fc2.
+
+Activations stay u8 NHWC in HBM between layers; nothing is staged through the
+host.  A forward at a fixed batch can be captured into a HIP graph
+(``capture_graph``) so a step is one graph launch.
+
+Reference interfaces mirrored: SURVEY.md §8(a) A0-A11; the quantize() flow of
+/root/reference/models/custom_quantization_model.py:169-195 (eval, cpu, fold)
+plus torch.ao prepare/convert with MinMax observers (observer.py:349-427).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from . import quant as Q
+
+F32 = np.float32
+CONV_TABLE = ((3, 64, False), (64, 64, True), (64, 128, False), (128, 128, True),
+              (128, 256, False), (256, 256, True))
+
+
+# ============================================================ fp32 folding
+def fold_state_dict(sd):
+    """BN-fold a SimpleConvNet state_dict (fuse_modules of
+    custom_quantization_model.py:180-190): conv_i+bn_i, fc1+bn7; fc2 as is."""
+    g = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in sd.items()}
+    out = {}
+    for i in range(1, 7):
+        out[f"conv{i}.w"], out[f"conv{i}.b"] = Q.fold_bn(
+            g[f"conv{i}.weight"], g.get(f"conv{i}.bias"), g[f"bn{i}.running_mean"],
+            g[f"bn{i}.running_var"], g[f"bn{i}.weight"], g[f"bn{i}.bias"])
+    out["fc1.w"], out["fc1.b"] = Q.fold_linear_bn(
+        g["fc1.weight"], g.get("fc1.bias"), g["bn7.running_mean"], g["bn7.running_var"],
+        g["bn7.weight"], g["bn7.bias"])
+    out["fc2.w"] = np.asarray(g["fc2.weight"], F32)
+    out["fc2.b"] = np.asarray(g["fc2.bias"], F32)
+    return out
+
+
+# ============================================================ calibration
+class _Range:
+    """Running min/max of one activation; device observer kernel on GPU,
+    torch.aminmax on CPU (observer.py:558-569)."""
+
+    def __init__(self, device):
+        self.dev = torch.device(device)
+        self.obs = ops.MinMaxObserver(self.dev) if self.dev.type == "cuda" else None
+        self.lo, self.hi = np.float32(np.inf), np.float32(-np.inf)
+
+    def __call__(self, x):
+        if x.numel() == 0:
+            return
+        if self.obs is not None:
+            self.obs(x.contiguous())
+        else:
+            lo, hi = torch.aminmax(x.detach())
+            self.lo = min(self.lo, np.float32(lo.item()))
+            self.hi = max(self.hi, np.float32(hi.item()))
+
+    def values(self):
+        return self.obs.values() if self.obs is not None else (self.lo, self.hi)
+
+
+def calibrate(folded, batches, device="cpu"):
+    """Run the BN-folded fp32 net over calibration batches and record the
+    ranges every observer of the static and the QDQ configuration needs."""
+    dev = torch.device(device)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in folded.items()}
+    names = ["x"] + [f"conv{i}_{s}" for i in range(1, 7) for s in ("in", "out")] + \
+        ["fc1_in", "fc1_out", "fc2_out"]
+    rng = {n: _Range(dev) for n in names}
+    with torch.no_grad():
+        for xb in batches:
+            x = xb.to(dev, torch.float32)
+            rng["x"](x)
+            for i, (_, _, pool) in enumerate(CONV_TABLE, start=1):
+                rng[f"conv{i}_in"](x)
+                x = F.conv2d(x, t[f"conv{i}.w"], t[f"conv{i}.b"], padding=1)
+                rng[f"conv{i}_out"](x)
+                x = F.relu(x)
+                if pool:
+                    x = F.max_pool2d(x, 2, 2)
+            x = x.reshape(x.shape[0], -1)
+            rng["fc1_in"](x)
+            x = F.linear(x, t["fc1.w"], t["fc1.b"])
+            rng["fc1_out"](x)
+            x = F.relu(x)
+            x = F.linear(x, t["fc2.w"], t["fc2.b"])
+            rng["fc2_out"](x)
+    return {n: r.values() for n, r in rng.items()}
+
+
+def _relu_range(lo_hi):
+    lo, hi = lo_hi
+    return max(F32(lo), F32(0.0)), max(F32(hi), F32(0.0))
+
+
+def _weight_scale(w, per_channel):
+    if per_channel:
+        flat = w.reshape(w.shape[0], -1)
+        return Q.qparams_symmetric(flat.min(1), flat.max(1))
+    return Q.qparams_symmetric(w.min(), w.max())
+
+
+def build_qspec(folded, ranges, mode="static", per_channel=False):
+    """Host quantized-model description (numpy) from folded fp32 weights and
+    observed ranges.  Layer entries: w (s8 OIHW / OI), b, s_w, s_x, z_x, s_y,
+    z_y, relu (+ next (s2, z2) for the QDQ hand-off)."""
+    spec = {"mode": mode, "per_channel": bool(per_channel)}
+    if mode == "static":
+        s_in, z_in = Q.qparams_affine(*ranges["x"])
+        spec["in"] = (s_in, z_in)
+        s_x, z_x = s_in, z_in
+        for i in range(1, 7):
+            w = folded[f"conv{i}.w"]
+            s_w = _weight_scale(w, per_channel)
+            s_y, z_y = Q.qparams_affine(*_relu_range(ranges[f"conv{i}_out"]))
+            spec[f"conv{i}"] = dict(w=Q.quantize_weight(w, s_w), b=folded[f"conv{i}.b"], s_w=s_w,
+                                    s_x=s_x, z_x=z_x, s_y=s_y, z_y=z_y, relu=True)
+            s_x, z_x = s_y, z_y
+        w = folded["fc1.w"]
+        s_w = _weight_scale(w, per_channel)
+        s_y, z_y = Q.qparams_affine(*_relu_range(ranges["fc1_out"]))
+        spec["fc1"] = dict(w=Q.quantize_weight(w, s_w), b=folded["fc1.b"], s_w=s_w, s_x=s_x,
+                           z_x=z_x, s_y=s_y, z_y=z_y, relu=True)
+        w = folded["fc2.w"]
+        s_w = _weight_scale(w, per_channel)
+        s_y2, z_y2 = Q.qparams_affine(*ranges["fc2_out"])
+        spec["fc2"] = dict(w=Q.quantize_weight(w, s_w), b=folded["fc2.b"], s_w=s_w, s_x=s_y,
+                           z_x=z_y, s_y=s_y2, z_y=z_y2, relu=False)
+    elif mode == "qdq":
+        for i in range(1, 7):
+            w = folded[f"conv{i}.w"]
+            s_w = _weight_scale(w, per_channel)
+            s_x, z_x = Q.qparams_affine(*ranges[f"conv{i}_in"])
+            s_y, z_y = Q.qparams_affine(*ranges[f"conv{i}_out"])
+            spec[f"conv{i}"] = dict(w=Q.quantize_weight(w, s_w), b=folded[f"conv{i}.b"], s_w=s_w,
+                                    s_x=s_x, z_x=z_x, s_y=s_y, z_y=z_y, relu=False)
+        w = folded["fc1.w"]
+        s_w = _weight_scale(w, per_channel)
+        s_x, z_x = Q.qparams_affine(*ranges["fc1_in"])
+        s_y, z_y = Q.qparams_affine(*ranges["fc1_out"])
+        spec["fc1"] = dict(w=Q.quantize_weight(w, s_w), b=folded["fc1.b"], s_w=s_w, s_x=s_x,
+                           z_x=z_x, s_y=s_y, z_y=z_y, relu=False)
+        spec["fc2"] = dict(w=folded["fc2.w"], b=folded["fc2.b"])
+        for i in range(1, 6):
+            spec[f"conv{i}"]["next"] = (spec[f"conv{i + 1}"]["s_x"], spec[f"conv{i + 1}"]["z_x"])
+        spec["conv6"]["next"] = (spec["fc1"]["s_x"], spec["fc1"]["z_x"])
+    else:
+        raise ValueError(f"unknown mode {mode!r}")
+    return spec
+
+
+def qspec_from_torch_ao(q):
+    """Import a torch.ao-converted full-int8 SimpleConvNet (quant stub, fused
+    Conv(ReLU)2d conv1..conv6, LinearReLU fc1, Linear fc2) — the model a
+    reference user builds with prepare/convert — into a static qspec."""
+    spec = {"mode": "static", "per_channel": False,
+            "in": (F32(q.quant.scale.item()), int(q.quant.zero_point.item()))}
+    s_x, z_x = spec["in"]
+    for name in [f"conv{i}" for i in range(1, 7)] + ["fc1", "fc2"]:
+        m = getattr(q, name)
+        wq = m.weight()
+        if wq.qscheme() in (torch.per_tensor_symmetric, torch.per_tensor_affine):
+            s_w = F32(wq.q_scale())
+        else:
+            s_w = wq.q_per_channel_scales().numpy().astype(F32)
+            spec["per_channel"] = True
+        spec[name] = dict(w=wq.int_repr().numpy(), b=m.bias().detach().numpy().astype(F32), s_w=s_w,
+                          s_x=s_x, z_x=z_x, s_y=F32(m.scale), z_y=int(m.zero_point),
+                          relu=name != "fc2")
+        s_x, z_x = F32(m.scale), int(m.zero_point)
+    return spec
+
+
+# ============================================================ device model
+class _DevLayer:
+    pass
+
+
+class QuantizedConvNet:
+    """Duck-typed int8 model object (the surface of the reference's models.*:
+    eval(), to() in place, cpu(), __call__; fp32 [N,3,32,32] in, fp32 [N,10] out)."""
+
+    def __init__(self, spec, device="cuda"):
+        self.spec = spec
+        self.mode = spec["mode"]
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the int8 path runs on the GPU (HIP); pass a cuda device")
+        self.quantized = True
+        self.is_custom_quantized = self.mode == "qdq"
+        self.host_io = False
+        self._bufs = {}
+        self._graphs = {}
+        self._upload()
+
+    # --------------------------------------------------------------- setup
+    def _t(self, a, dtype=None):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if dtype is not None:
+            t = t.to(dtype)
+        return t.to(self.device)
+
+    def _upload(self):
+        sp = self.spec
+        self.L = []
+        for i, (cin, cout, pool) in enumerate(CONV_TABLE, start=1):
+            e = sp[f"conv{i}"]
+            d = _DevLayer()
+            d.cin, d.cout, d.pool, d.relu = cin, cout, pool, e["relu"]
+            if i == 1:
+                packed, wsum = ops.pack_conv1(e["w"])
+            else:
+                packed, wsum = ops.pack_conv3x3(e["w"])
+            u, v, mult = Q.epilogue_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
+            d.w = self._t(packed)
+            d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
+            d.corr = self._t(((128 - int(e["z_x"])) * wsum.astype(np.int64)).astype(np.int32))
+            d.z_x, d.z_y, d.s_x, d.s_y = int(e["z_x"]), int(e["z_y"]), F32(e["s_x"]), F32(e["s_y"])
+            d.qdq = ops.qdq_struct(e["s_y"], e["z_y"], *e["next"]) if "next" in e else None
+            self.L.append(d)
+        if self.mode == "static":
+            self.in_scale, self.in_zp = sp["in"]
+        else:
+            self.in_scale, self.in_zp = sp["conv1"]["s_x"], sp["conv1"]["z_x"]
+        perm = Q.nhwc_flatten_perm()
+        for name in ("fc1", "fc2"):
+            e = sp[name]
+            d = _DevLayer()
+            if self.mode == "qdq" and name == "fc2":
+                d.w = self._t(np.asarray(e["w"], F32))
+                d.b = self._t(np.asarray(e["b"], F32))
+                setattr(self, name, d)
+                continue
+            w = np.asarray(e["w"], np.int8)
+            if name == "fc1":
+                w = np.ascontiguousarray(w[:, perm])  # NHWC flatten order
+            wsum = w.astype(np.int64).sum(1)
+            u, v, mult = Q.epilogue_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
+            d.w = self._t(w)
+            d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
+            d.corr = self._t(((128 - int(e["z_x"])) * wsum).astype(np.int32))
+            d.z_x, d.z_y, d.s_y, d.relu = int(e["z_x"]), int(e["z_y"]), F32(e["s_y"]), e["relu"]
+            setattr(self, name, d)
+
+    def _buffers(self, n):
+        b = self._bufs.get(n)
+        if b is None:
+            dev = self.device
+            b = {"a1": torch.empty((n, 32, 32, 64), dtype=torch.uint8, device=dev),
+                 "a2": torch.empty((n, 16, 16, 64), dtype=torch.uint8, device=dev),
+                 "a3": torch.empty((n, 16, 16, 128), dtype=torch.uint8, device=dev),
+                 "a4": torch.empty((n, 8, 8, 128), dtype=torch.uint8, device=dev),
+                 "a5": torch.empty((n, 8, 8, 256), dtype=torch.uint8, device=dev),
+                 "a6": torch.empty((n, 4, 4, 256), dtype=torch.uint8, device=dev),
+                 "f1": torch.empty((n, 512), dtype=torch.uint8, device=dev),
+                 "f1f": torch.empty((n, 512), dtype=torch.float32, device=dev),
+                 "q": torch.empty((n, 10), dtype=torch.uint8, device=dev),
+                 "logits": torch.empty((n, 10), dtype=torch.float32, device=dev)}
+            self._bufs[n] = b
+        return b
+
+    # --------------------------------------------------------------- forward
+    def run(self, x, keep=False):
+        """Launch the whole int8 forward on the current stream (no sync).
+        Returns the fp32 logits tensor (a reused buffer); with keep=True also
+        the dict of intermediate u8 activations."""
+        n = x.shape[0]
+        b = self._buffers(n)
+        L = self.L
+        d = L[0]
+        ops.conv1_f32(x, self.in_scale, self.in_zp, d.w, d.u, d.v, d.mult, d.corr, d.z_y, d.relu,
+                      d.qdq, out=b["a1"])
+        prev = b["a1"]
+        names = ["a2", "a3", "a4", "a5", "a6"]
+        for i in range(1, 6):
+            d = L[i]
+            ops.conv3x3(prev, d.z_x, d.w, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, d.pool,
+                        d.qdq, out=b[names[i - 1]])
+            prev = b[names[i - 1]]
+        flat = prev.view(n, 4096)
+        f1, f2 = self.fc1, self.fc2
+        if self.mode == "static":
+            ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, True,
+                          out=b["f1"])
+            ops.linear_u8(b["f1"], f2.z_x, f2.w, f2.u, f2.v, f2.mult, f2.corr, f2.z_y, False,
+                          y_scale=f2.s_y, want_fp32=True, out=b["q"], out_f=b["logits"])
+        else:
+            ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, False,
+                          y_scale=f1.s_y, want_fp32=True, out=b["f1"], out_f=b["f1f"])
+            ops.linear_f32(b["f1f"], f2.w, f2.b, relu_in=True, out=b["logits"])
+        if keep:
+            return b["logits"], b
+        return b["logits"]
+
+    def capture_graph(self, x_static):
+        """Capture run(x_static) into a HIP graph; replay with replay(n)."""
+        n = x_static.shape[0]
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.run(x_static)  # warm-up: kernel attributes, buffers
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self.run(x_static)
+        self._graphs[n] = (g, x_static, out)
+        return g
+
+    def replay(self, n):
+        g, _, out = self._graphs[n]
+        g.replay()
+        return out
+
+    @torch.no_grad()
+    def forward(self, x):
+        host = not x.is_cuda
+        xd = x.to(self.device, torch.float32, non_blocking=False).contiguous()
+        out = self.run(xd).clone()
+        if host or self.host_io:
+            return out.cpu()
+        # the reference harness times model(data) with time.time() and no device
+        # sync (utils/inference_benchmark.py:94-98): finish the work here.
+        torch.cuda.current_stream(self.device).synchronize()
+        return out
+
+    __call__ = forward
+
+    # ------------------------------------------------- nn.Module-like surface
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise RuntimeError("QuantizedConvNet is inference-only")
+        return self
+
+    def to(self, device):
+        dev = torch.device(device)
+        if dev.type == "cpu":
+            self.host_io = True   # compute stays on the GPU; I/O is host tensors
+        return self
+
+    def cpu(self):
+        """The reference evaluator calls model.cpu() and feeds CPU tensors
+        (utils/model_evaluator.py:20,30-31): keep compute on the GPU and accept /
+        return host tensors."""
+        self.host_io = True
+        return self
+
+    def cuda(self, device=None):
+        self.host_io = False
+        return self
+
+    def state_dict(self):
+        return {k: v for k, v in self.spec.items()}
+
+    def model_size_bytes(self):
+        total = 0
+        for name in [f"conv{i}" for i in range(1, 7)] + ["fc1", "fc2"]:
+            e = self.spec[name]
+            total += np.asarray(e["w"]).nbytes + np.asarray(e["b"]).nbytes
+        return total

@@ -1,0 +1,134 @@
+/*
+ * qconvnet.h — C ABI of the MI355X (gfx950) int8 ConvNet inference path.
+ *
+ * One shared library, libqconvnet.so, built from
+ * the HIP sources in convnet-quantization_amd/csrc/.  Every compute entry point:
+ *   - takes caller-owned DEVICE pointers (e.g. torch tensors' data_ptr()),
+ *     explicit shapes and quantization parameters, and an explicit HIP
+ *     stream (hipStream_t passed as void*; NULL = default stream);
+ *   - allocates nothing and never synchronizes (safe inside hipGraph capture);
+ *   - returns 0 (QCN_OK) or a negative status; no exceptions cross the ABI.
+ * The qcn_pack_* functions work on HOST memory (one-time weight packing).
+ *
+ * The reference (his0si/ConvNet-Quantization) has no FFI: its hot path is the
+ * torch.ao / FBGEMM arithmetic behind its duck-typed model objects.  Each entry
+ * below names the reference interface it replaces (file:line in
+ * /root/reference unless prefixed torch/, which is the torch 2.10 wheel).
+ * Numerics are bit-exact with torch.ao's fbgemm engine on the integer path
+ * (see oracle/qref.py and tests/golden/).
+ */
+#ifndef QCONVNET_H
+#define QCONVNET_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QCN_OK 0
+#define QCN_ERR_ARG (-1)          /* invalid argument / shape                     */
+#define QCN_ERR_UNSUPPORTED (-2)  /* shape combination has no kernel              */
+#define QCN_ERR_HIP (-3)          /* HIP launch / runtime error                   */
+
+/* Per-layer QDQ hand-off (CustomQuantizedConv2d chain): after requantizing to
+ * (scale s1, zero point z1), dequantize, ReLU, and quantize with the next
+ * layer's input qparams (inv2 = fp32(1/scale2), z2).  Replaces the fp32
+ * DeQuantStub -> F.relu -> [pool] -> QuantStub sequence of
+ * models/custom_quantization_model.py:41-45, :237-252. */
+typedef struct qcn_qdq_t {
+  float s1;
+  int32_t z1;
+  float inv2;
+  int32_t z2;
+} qcn_qdq_t;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int qcn_version(void);
+
+/* A1 — aten::quantize_per_tensor (QuantStub once converted,
+ * models/custom_quantization_model.py:42,55,234):
+ *   q = clamp(zp + rne(x * fp32(1/scale)), 0, 255).
+ * x is fp32 [n,c,h,w] NCHW; q is u8, NHWC when nhwc_out != 0 else NCHW. */
+int qcn_quantize_f32_u8(const float* x, uint8_t* q, int n, int c, int h, int w, int nhwc_out,
+                        float scale, int zero_point, void* stream);
+
+/* A7 — aten::dequantize (DeQuantStub, custom_quantization_model.py:44,57,260):
+ *   x = fp32(scale) * fp32(q - zp). */
+int qcn_dequantize_u8_f32(const uint8_t* q, float* x, long long count, float scale,
+                          int zero_point, void* stream);
+
+/* A2 — MinMaxObserver.forward (torch/ao/quantization/observer.py:558-569):
+ * running [min, max] of fp32 data, reduced on the device.  minmax points to 2
+ * device floats; qcn_minmax_reset writes [+inf, -inf]. */
+int qcn_minmax_reset(float* minmax, void* stream);
+int qcn_minmax_f32(const float* x, long long count, float* minmax, void* stream);
+
+/* A10 — nn.MaxPool2d(2, 2) on u8 NHWC (baseline_model.py:17,25,33). */
+int qcn_maxpool2x2_u8_nhwc(const uint8_t* x, int n, int h, int w, int c, uint8_t* y,
+                           void* stream);
+
+/* A11 — argmax over the last axis, ties -> lowest index (torch.argmax /
+ * topk(1), utils/model_evaluator.py:36,96,160). */
+int qcn_argmax_f32(const float* x, int rows, int cols, long long* idx, void* stream);
+
+/* A5/A6 weight packing (host).  w_oihw is torch's s8 [cout][cin][3][3].
+ * out receives qcn_conv3x3_packed_size(cin, cout) bytes; wsum[cout] receives
+ * sum_k w (for the activation zero-point correction). */
+int qcn_conv3x3_packed_size(int cin, int cout);
+int qcn_pack_conv3x3_weight(const int8_t* w_oihw, int cout, int cin, int8_t* out, int32_t* wsum);
+int qcn_pack_conv1_weight(const int8_t* w_oihw, int cout, int8_t* out, int32_t* wsum);
+
+/* A5/A6/A10 — QuantizedConv2d / QuantizedConvReLU2d (fbgemm), 3x3, pad 1,
+ * stride 1, optionally followed by a fused 2x2 max-pool and a per-layer QDQ
+ * hand-off (qdq may be NULL).  Replaces the conv of CustomQuantizedConv2d
+ * (custom_quantization_model.py:43) and the FX/eager full-int8 conv.
+ *   x: u8 NHWC [nimg,h,w,cin] (zero point x_zp);  y: u8 NHWC.
+ *   u, v, mult: fp32 [cout] epilogue constants (t = fmaf(u,v,acc); ab = t*mult)
+ *   corr: int32 [cout] = (128 - x_zp) * wsum  (activations enter the MFMA as
+ *   q - 128). */
+int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                          const int8_t* w_packed, int cout, const float* u, const float* v,
+                          const float* mult, const int32_t* corr, int y_zp, int relu, int pool,
+                          const qcn_qdq_t* qdq, uint8_t* y, void* stream);
+
+/* A1+A5+A6 fused — QuantStub + conv1(+ReLU) of SimpleConvNet
+ * (baseline_model.py:13, :60): fp32 NCHW [nimg,3,hw,hw] in, quantized with
+ * (in_scale, in_zp), 3x3 conv to 64 channels, u8 NHWC out.  q_in (optional,
+ * may be NULL) receives the quantized input, u8 NHWC. */
+int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_zp,
+                       const int8_t* w1_packed, const float* u, const float* v, const float* mult,
+                       const int32_t* corr, int y_zp, int relu, const qcn_qdq_t* qdq, uint8_t* y,
+                       uint8_t* q_in, void* stream);
+
+/* A9 — quantized Linear / LinearReLU (fbgemm), static qparams:
+ * fc1/fc2 of SimpleConvNet (baseline_model.py:38,40).
+ *   x: u8 [m,k] (zero point x_zp); w: s8 [n,k] row-major; y: u8 [m,n].
+ *   y_deq (optional) receives fp32 (y - y_zp) * y_scale  (DeQuantStub). */
+int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, int n,
+                    const float* u, const float* v, const float* mult, const int32_t* corr,
+                    int y_zp, int relu, uint8_t* y, float* y_deq, float y_scale, void* stream);
+
+/* A8 — quantized::linear_dynamic (DynamicQuantizedLinear of
+ * models/static_ptq_model.py:28-32 and models/dynamic_ptq_model.py:302-306):
+ * per-call activation qparams from the batch min/max (ChooseQuantizationParams,
+ * qrange [0,127] when reduce_range), quantize, u8 x s8 GEMM,
+ * y = fmaf(fp32(acc), fp32(s_x * s_w), bias).  w_scale holds 1 (per-tensor) or
+ * n (per-channel) floats; bias may be NULL.  workspace: >= 64 bytes of device
+ * memory + m*k bytes (quantized activations). */
+long long qcn_linear_dynamic_workspace_size(int m, int k);
+int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
+                           const float* w_scale, int per_channel, const int32_t* wsum,
+                           const float* bias, int reduce_range, float* y, void* workspace,
+                           void* stream);
+
+/* fp32 Linear (fc2 of CustomQuantizedSimpleConvNet stays fp32,
+ * custom_quantization_model.py:219): y = x @ w^T + b, with optional ReLU on x
+ * (relu_in) applied on load. */
+int qcn_linear_f32(const float* x, int m, int k, const float* w, int n, const float* b,
+                   int relu_in, float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QCONVNET_H */

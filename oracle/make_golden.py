@@ -276,7 +276,7 @@ def gen_net(per_channel=False, batch=64):
         rec[f"bn{i}_var"] = sd[f"bn{i}.running_var"].numpy()
     # quantized parameters: scales/zps in full, int8 weights by hash
     for k, v in qm.items():
-        if k.endswith("_w"):
+        if k.endswith("_w") and not k.endswith("_s_w"):
             rec[k + "_sha"] = sha(v)
         else:
             rec["qm_" + k] = np.asarray(v)

@@ -101,7 +101,18 @@ def fold_conv_bn(w, b, rm, rv, gamma, beta, eps=1e-5):
     return wf, bf
 
 
-fold_linear_bn = fold_conv_bn  # fusion.py:156-186 is the same arithmetic
+def fold_linear_bn(w, b, rm, rv, gamma, beta, eps=1e-5):
+    """torch.nn.utils.fusion.fuse_linear_bn_weights (fusion.py:156-186): unlike
+    the conv fold the bias uses the combined scale:
+    s = gamma * rsqrt(var+eps); w' = w * s; b' = (b - mean) * s + beta."""
+    w = np.asarray(w, F32)
+    if b is None:
+        b = np.zeros(w.shape[0], F32)
+    rsq = F32(1.0) / np.sqrt(np.asarray(rv, F32) + F32(eps))
+    s = (np.asarray(gamma, F32) * rsq).astype(F32)
+    wf = (w * s.reshape(-1, 1)).astype(F32)
+    bf = (((np.asarray(b, F32) - np.asarray(rm, F32)) * s) + np.asarray(beta, F32)).astype(F32)
+    return wf, bf
 
 
 # --------------------------------------------------------------------------- A4

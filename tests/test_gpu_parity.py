@@ -1,0 +1,267 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the committed
+torch.ao/fbgemm golden vectors and the numpy oracle.  Integer outputs must be
+bit-exact; fp32 outputs that follow the same fp32 op order are compared
+exactly too (dequantize, dynamic Linear); only the fp32 fc2 of the QDQ model
+(a plain fp32 GEMM, summation order differs from MKL) uses a tolerance."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import qref
+
+pytestmark = pytest.mark.gpu
+
+F32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from qconvnet import _lib
+    _lib.load()  # fail loudly if the HIP library is missing
+    return torch.device("cuda:0")
+
+
+def _g(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name)))
+
+
+def test_quantize_dequantize_golden(dev, golden_dir):
+    from qconvnet import ops
+    z = _g(golden_dir, "ops_quantize.npz")
+    for i in range(5):
+        x = z[f"q{i}_x"]
+        n = x.size
+        xt = torch.from_numpy(x.reshape(1, 1, 1, n)).to(dev)
+        q = ops.quantize(xt, z[f"q{i}_scale"], int(z[f"q{i}_zp"]), nhwc=False)
+        assert np.array_equal(q.cpu().numpy().reshape(-1), z[f"q{i}_q"]), i
+        dq = ops.dequantize(q, z[f"q{i}_scale"], int(z[f"q{i}_zp"]))
+        assert np.array_equal(dq.cpu().numpy().reshape(-1), z[f"q{i}_dq"]), i
+
+
+def test_quantize_nchw_to_nhwc(dev):
+    from qconvnet import ops
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((5, 3, 7, 9)) * 2).astype(F32)
+    q = ops.quantize(torch.from_numpy(x).to(dev), F32(0.02), 117, nhwc=True)
+    ref = qref.quantize_per_tensor(np.transpose(x, (0, 2, 3, 1)), F32(0.02), 117)
+    assert np.array_equal(q.cpu().numpy(), ref)
+
+
+def test_minmax_observer(dev):
+    from qconvnet import ops
+    rng = np.random.default_rng(4)
+    obs = ops.MinMaxObserver(dev)
+    lo, hi = np.inf, -np.inf
+    for n in (1, 3, 1000, 12345, 1 << 20):
+        x = (rng.standard_normal(n) * rng.uniform(0.1, 10)).astype(F32)
+        obs(torch.from_numpy(x).to(dev))
+        lo, hi = min(lo, x.min()), max(hi, x.max())
+        got = obs.values()
+        assert got[0] == F32(lo) and got[1] == F32(hi)
+    # misaligned view + all-negative data
+    x = -np.abs(rng.standard_normal(1001)).astype(F32) - 1
+    obs.reset()
+    obs(torch.from_numpy(x).to(dev)[1:])
+    assert obs.values() == (F32(x[1:].min()), F32(x[1:].max()))
+
+
+def test_maxpool_argmax(dev):
+    from qconvnet import ops
+    rng = np.random.default_rng(5)
+    for c in (16, 64, 3):
+        q = rng.integers(0, 256, (3, 8, 6, c)).astype(np.uint8)
+        got = ops.maxpool2x2(torch.from_numpy(q).to(dev)).cpu().numpy()
+        assert np.array_equal(got, qref.maxpool2x2_nhwc(q))
+    x = rng.integers(0, 4, (257, 10)).astype(F32)  # many ties
+    got = ops.argmax(torch.from_numpy(x).to(dev)).cpu().numpy()
+    assert np.array_equal(got, qref.argmax_rows(x))
+
+
+def _conv_case(z, i):
+    g = lambda k: z[f"c{i}_{k}"]  # noqa: E731
+    return {k: g(k) for k in ("qx", "zx", "s_x", "w", "s_w", "b", "s_y", "zy", "relu", "out")}
+
+
+def _run_conv(dev, c, pool=False, qdq=None):
+    from qconvnet import ops, quant as Q
+    w_oihw = np.ascontiguousarray(c["w"].transpose(0, 3, 1, 2))
+    packed, wsum = ops.pack_conv3x3(w_oihw)
+    u, v, mult = Q.epilogue_constants(c["s_x"], c["s_w"] if c["s_w"].size > 1 else c["s_w"].reshape(-1)[0],
+                                      c["s_y"], c["b"])
+    corr = ((128 - int(c["zx"])) * wsum.astype(np.int64)).astype(np.int32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    y = ops.conv3x3(T(c["qx"]), int(c["zx"]), T(packed), w_oihw.shape[0], T(u), T(v), T(mult),
+                    T(corr), int(c["zy"]), bool(c["relu"]), pool, qdq)
+    return y.cpu().numpy()
+
+
+def test_conv_golden(dev, golden_dir):
+    z = _g(golden_dir, "ops_conv.npz")
+    for i in range(int(z["n"])):
+        c = _conv_case(z, i)
+        got = _run_conv(dev, c)
+        assert np.array_equal(got, c["out"]), f"case {i}: {(got != c['out']).sum()} mismatches"
+
+
+@pytest.mark.parametrize("n,h,cin,cout,pool,zx", [
+    (3, 32, 64, 64, True, 0), (2, 32, 64, 64, False, 7), (3, 16, 64, 128, False, 0),
+    (2, 16, 128, 128, True, 3), (5, 8, 128, 256, False, 0), (5, 8, 256, 256, True, 250),
+    (3, 4, 256, 256, True, 0), (1, 6, 64, 64, False, 9), (2, 8, 192, 64, True, 1)])
+def test_conv_tuned_vs_oracle(dev, n, h, cin, cout, pool, zx):
+    """Every tuned instantiation (and the generic fallback) against the oracle,
+    full-range u8 inputs, partial workgroups (odd image counts)."""
+    from qconvnet import ops, quant as Q
+    rng = np.random.default_rng(n * 1000 + h * 10 + cin + cout)
+    qx = rng.integers(0, 256, (n, h, h, cin)).astype(np.uint8)
+    w = rng.integers(-127, 128, (cout, cin, 3, 3)).astype(np.int8)
+    b = (rng.standard_normal(cout) * 2).astype(F32)
+    s_x, s_w, s_y, zy = F32(0.02), F32(0.003), F32(rng.uniform(0.5, 3)), int(rng.integers(0, 60))
+    c = dict(qx=qx, zx=np.int64(zx), s_x=s_x, w=np.ascontiguousarray(w.transpose(0, 2, 3, 1)),
+             s_w=np.asarray(s_w), b=b, s_y=s_y, zy=np.int64(zy), relu=np.int64(1))
+    got = _run_conv(dev, c, pool=pool)
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    ref = qref.requantize(qref.conv3x3_acc_nhwc(qx, zx, c["w"]) if not pool else
+                          _pool_acc(qref.conv3x3_acc_nhwc(qx, zx, c["w"])), u, v, mult, zy, True)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} mismatches"
+
+
+def _pool_acc(acc):
+    n, h, w, c = acc.shape
+    return acc.reshape(n, h // 2, 2, w // 2, 2, c).max(axis=(2, 4))
+
+
+def test_conv_qdq_handoff(dev):
+    """Per-layer QDQ epilogue == requant -> dequant -> relu -> quantize(next)."""
+    from qconvnet import ops
+    rng = np.random.default_rng(11)
+    n, h, cin, cout = 2, 16, 64, 128
+    qx = rng.integers(0, 256, (n, h, h, cin)).astype(np.uint8)
+    w = rng.integers(-100, 101, (cout, cin, 3, 3)).astype(np.int8)
+    b = (rng.standard_normal(cout)).astype(F32)
+    c = dict(qx=qx, zx=np.int64(17), s_x=F32(0.02), w=np.ascontiguousarray(w.transpose(0, 2, 3, 1)),
+             s_w=np.asarray(F32(0.002)), b=b, s_y=F32(1.5), zy=np.int64(131), relu=np.int64(0))
+    s2, z2 = F32(0.9), 5
+    got = _run_conv(dev, c, qdq=ops.qdq_struct(c["s_y"], 131, s2, z2))
+    u, v, mult = qref.requant_constants(c["s_x"], c["s_w"], c["s_y"], b)
+    q1 = qref.requantize(qref.conv3x3_acc_nhwc(qx, 17, c["w"]), u, v, mult, 131, False)
+    x1 = np.maximum(qref.dequantize(q1, c["s_y"], 131), F32(0))
+    ref = qref.quantize_per_tensor(x1, s2, z2)
+    assert np.array_equal(got, ref)
+
+
+def test_conv1_fused_quantize(dev):
+    from qconvnet import ops, quant as Q
+    rng = np.random.default_rng(12)
+    for n, hw in ((3, 32), (5, 16), (9, 8)):
+        x = (rng.standard_normal((n, 3, hw, hw)) * 1.3).astype(F32)
+        w = rng.integers(-127, 128, (64, 3, 3, 3)).astype(np.int8)
+        b = rng.standard_normal(64).astype(F32)
+        s_in, z_in, s_w, s_y = F32(0.021), 121, F32(0.004), F32(0.05)
+        packed, wsum = ops.pack_conv1(w)
+        u, v, mult = Q.epilogue_constants(s_in, s_w, s_y, b)
+        corr = ((128 - z_in) * wsum.astype(np.int64)).astype(np.int32)
+        T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        qin = torch.empty((n, hw, hw, 3), dtype=torch.uint8, device=dev)
+        y = ops.conv1_f32(T(x), s_in, z_in, T(packed), T(u), T(v), T(mult), T(corr), 0, True,
+                          q_in=qin).cpu().numpy()
+        q_ref = qref.quantize_per_tensor(qref.nchw_to_nhwc(x), s_in, z_in)
+        assert np.array_equal(qin.cpu().numpy(), q_ref)
+        u2, v2, m2 = qref.requant_constants(s_in, s_w, s_y, b)
+        ref = qref.conv3x3_q(q_ref, z_in, np.ascontiguousarray(w.transpose(0, 2, 3, 1)), u2, v2, m2,
+                             0, True)
+        assert np.array_equal(y, ref), f"{(y != ref).sum()} mismatches"
+
+
+def test_linear_golden(dev, golden_dir):
+    from qconvnet import ops, quant as Q
+    z = _g(golden_dir, "ops_linear.npz")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    for i in range(int(z["n"])):
+        g = lambda k: z[f"l{i}_{k}"]  # noqa: E731
+        w = g("w")
+        wsum = w.astype(np.int64).sum(1)
+        u, v, mult = Q.epilogue_constants(g("s_x"), g("s_w"), g("s_y"), g("b"))
+        corr = ((128 - int(g("zx"))) * wsum).astype(np.int32)
+        y, yf = ops.linear_u8(T(g("qx")), int(g("zx")), T(w), T(u), T(v), T(mult), T(corr),
+                              int(g("zy")), bool(g("relu")), y_scale=g("s_y"), want_fp32=True)
+        assert np.array_equal(y.cpu().numpy(), g("out")), i
+        assert np.array_equal(yf.cpu().numpy(), qref.dequantize(g("out"), g("s_y"), int(g("zy"))))
+
+
+def test_linear_dynamic_golden(dev, golden_dir):
+    from qconvnet import ops
+    z = _g(golden_dir, "ops_dynamic_linear.npz")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    for i in range(int(z["n"])):
+        w = z[f"d{i}_w"]
+        wsum = w.astype(np.int64).sum(1).astype(np.int32)
+        y = ops.linear_dynamic(T(z[f"d{i}_x"]), T(w), T(np.atleast_1d(z[f"d{i}_s_w"])), T(wsum),
+                               T(z[f"d{i}_b"]))
+        got = y.cpu().numpy()
+        assert np.array_equal(got, z[f"d{i}_y"]), f"case {i}: {(got != z[f'd{i}_y']).sum()}"
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_full_net_static_int8_golden(dev, per_channel):
+    """Whole static-int8 SimpleConvNet vs torch.ao (fbgemm): logits bit-exact,
+    every intermediate u8 activation bit-exact (by hash)."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load(per_channel)
+    spec, _ = netfix.static_spec(z)
+    assert netfix.check_weights(spec, z) == []
+    x = netfix.images(z)
+    model = QuantizedConvNet(spec, dev)
+    logits, bufs = model.run(torch.from_numpy(x).to(dev), keep=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(bufs["q"].cpu().numpy(), z["q_logits"])
+    assert np.array_equal(logits.cpu().numpy(), z["logits"])
+    for i, name in enumerate(["a1", "a2", "a3", "a4", "a5", "a6"], start=1):
+        assert netfix.sha(bufs[name].cpu().numpy()) == str(z[f"conv{i}_sha"]), name
+    assert netfix.sha(bufs["f1"].cpu().numpy()) == str(z["fc1_sha"])
+    assert np.array_equal(model(torch.from_numpy(x)).argmax(1).numpy(), z["argmax"])
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_full_net_qdq_golden(dev, per_channel):
+    """Per-layer QDQ model (reference CustomQuantizedSimpleConvNet with live
+    stubs): integer chain bit-exact, fp32 fc2 within 1e-5 relative."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load(per_channel)
+    spec = netfix.qdq_spec(z)
+    x = netfix.images(z)
+    model = QuantizedConvNet(spec, dev)
+    got = model(torch.from_numpy(x)).numpy()
+    ref = z["qdq_logits"]
+    tol = 1e-5 * np.abs(ref).max()
+    assert np.abs(got - ref).max() <= tol, np.abs(got - ref).max()
+    assert np.array_equal(got.argmax(1), ref.argmax(1))
+
+
+def test_batch_split_invariance_and_graph(dev):
+    """Static path is batch-independent: a 1024 batch equals its four 256
+    shards; the HIP-graph replay equals the eager launch sequence."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    from oracle import torch_ref
+    z = netfix.load(False)
+    spec, _ = netfix.static_spec(z)
+    model = QuantizedConvNet(spec, dev)
+    x = torch.from_numpy(torch_ref.synthetic_images(1024, 7)).to(dev)
+    full = model.run(x).clone()
+    parts = torch.cat([model.run(x[i * 256:(i + 1) * 256]).clone() for i in range(4)])
+    assert torch.equal(full, parts)
+    xs = x.clone()
+    model.capture_graph(xs)
+    out = model.replay(1024)
+    torch.cuda.synchronize()
+    assert torch.equal(out, full)
+    xs.copy_(torch.flip(x, [0]))
+    out = model.replay(1024)
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.flip(full, [0]))

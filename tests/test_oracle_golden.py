@@ -1,0 +1,89 @@
+"""CPU: the oracle (oracle/qref.py) against the committed torch.ao/fbgemm
+golden vectors — the pin that makes every GPU parity claim meaningful."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import qref
+
+F32 = np.float32
+
+
+def _g(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name)))
+
+
+def test_quantize_dequantize(golden_dir):
+    z = _g(golden_dir, "ops_quantize.npz")
+    for i in range(5):
+        q = qref.quantize_per_tensor(z[f"q{i}_x"], z[f"q{i}_scale"], int(z[f"q{i}_zp"]))
+        assert np.array_equal(q, z[f"q{i}_q"])
+        assert np.array_equal(qref.dequantize(q, z[f"q{i}_scale"], int(z[f"q{i}_zp"])), z[f"q{i}_dq"])
+
+
+def test_observer_qparams(golden_dir):
+    z = _g(golden_dir, "ops_qparams.npz")
+    for lo, hi, s, zp, ss in zip(z["min"], z["max"], z["aff_scale"], z["aff_zp"], z["sym_scale"]):
+        assert qref.qparams_affine(lo, hi) == (F32(s), int(zp))
+        assert qref.qparams_symmetric(lo, hi)[0] == F32(ss)
+
+
+def test_conv_requant(golden_dir):
+    z = _g(golden_dir, "ops_conv.npz")
+    for i in range(int(z["n"])):
+        g = lambda k: z[f"c{i}_{k}"]  # noqa: E731
+        s_w = g("s_w")
+        u, v, mult = qref.requant_constants(g("s_x"), s_w, g("s_y"), g("b"))
+        out = qref.conv3x3_q(g("qx"), int(g("zx")), g("w"), u, v, mult, int(g("zy")), bool(g("relu")))
+        assert np.array_equal(out, g("out")), i
+
+
+def test_linear_requant(golden_dir):
+    z = _g(golden_dir, "ops_linear.npz")
+    for i in range(int(z["n"])):
+        g = lambda k: z[f"l{i}_{k}"]  # noqa: E731
+        u, v, mult = qref.requant_constants(g("s_x"), g("s_w"), g("s_y"), g("b"))
+        out = qref.linear_q(g("qx"), int(g("zx")), g("w"), u, v, mult, int(g("zy")), bool(g("relu")))
+        assert np.array_equal(out, g("out")), i
+
+
+def test_dynamic_linear(golden_dir):
+    z = _g(golden_dir, "ops_dynamic_linear.npz")
+    for i in range(int(z["n"])):
+        y = qref.linear_dynamic(z[f"d{i}_x"], z[f"d{i}_w"], z[f"d{i}_s_w"], z[f"d{i}_b"])
+        assert np.array_equal(y, z[f"d{i}_y"]), i
+
+
+def test_fmaf_exact():
+    """The vectorised fmaf helper equals a single-rounding FMA: checked against
+    exact rational arithmetic on adversarial near-tie inputs."""
+    from fractions import Fraction
+    rng = np.random.default_rng(0)
+    a = rng.standard_normal(2000).astype(F32)
+    b = (np.ldexp(1.0, rng.integers(-30, 30, 2000)) * rng.uniform(1, 2, 2000)).astype(F32)
+    c = np.ldexp(rng.integers(-(1 << 24), 1 << 24, 2000).astype(np.float64), rng.integers(-5, 40, 2000)).astype(F32)
+    got = qref.fmaf(a, b, c)
+    for x, y, w, r in zip(a[:400], b[:400], c[:400], got[:400]):
+        exact = Fraction(float(x)) * Fraction(float(y)) + Fraction(float(w))
+        lo = np.float32(float(exact))
+        cands = [np.nextafter(lo, np.float32(-np.inf)), lo, np.nextafter(lo, np.float32(np.inf))]
+        best = min(cands, key=lambda f: (abs(Fraction(float(f)) - exact),
+                                          int(np.float32(f).view(np.int32)) & 1))
+        assert r == best
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_full_net_oracle(per_channel):
+    """Oracle whole-net forward with the product's host quantization of the
+    seeded weights == torch.ao logits (first 8 images: the static path is
+    batch-independent)."""
+    import netfix
+    z = netfix.load(per_channel)
+    spec, _ = netfix.static_spec(z)
+    assert netfix.check_weights(spec, z) == []
+    x = netfix.images(z)[:8]
+    logits, q, inter = qref.static_int8_forward(x, netfix.oracle_dict(spec), keep=True)
+    assert np.array_equal(q, z["q_logits"][:8])
+    assert np.array_equal(logits, z["logits"][:8])
+    assert np.array_equal(inter["conv1"][:2, :2, :2], z["conv1_slice"])
