@@ -1,0 +1,245 @@
+"""Benchmark: images/sec of the full static-PTQ int8 SimpleConvNet at batch 1024
+(3x32x32) per MI355X — BASELINE.json's metric on configs[2] (N=1) and
+configs[3] (batch 8192 = 8 x 1024 sharded, RCCL all-gather of logits, N=8).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A step = one forward of the whole int8 net over this rank's 1024 resident
+images (fp32 NCHW in HBM -> quantize+conv1 ... fc2 -> fp32 logits) plus, for
+N > 1, the all-gather of every rank's logits.  Weak scaling: 1024 images per
+GPU.  Weights: random-init SimpleConvNet with BN statistics recalibrated on
+synthetic CIFAR-normalised images (no trained checkpoint or dataset offline),
+calibrated once on rank 0 and broadcast.
+
+Prints ONE JSON line on rank 0 with value (whole-job images/sec), a
+``roofline`` object for the dominant kernel (HIP-event per-kernel timing over
+a second timed pass) and, at N = 1, ``cpu_baseline`` (the reference's
+StaticPTQModel path — torch.ao quantize_dynamic — timed on the host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "convnet-quantization_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec at batch 1024 (3×32×32) int8 static-PTQ, 1/2/4/8 MI355X; top-1 delta"
+PEAK_INT8_TOPS = 5033.0   # 256 CU x 4 SIMD x 2048 int8 op/clk x 2.4 GHz (dense)
+PEAK_HBM_GBS = 8000.0
+# MAC per image per kernel
+MAC_PER_IMAGE = {"conv1": 1_769_472, "conv2": 37_748_736, "conv3": 18_874_368,
+                 "conv4": 37_748_736, "conv5": 18_874_368, "conv6": 37_748_736,
+                 "fc1": 2_097_152, "fc2": 5_120}
+# algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
+BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
+                   "conv2": 32 * 32 * 64 + 16 * 16 * 64,
+                   "conv3": 16 * 16 * 64 + 16 * 16 * 128,
+                   "conv4": 16 * 16 * 128 + 8 * 8 * 128,
+                   "conv5": 8 * 8 * 128 + 8 * 8 * 256,
+                   "conv6": 8 * 8 * 256 + 4 * 4 * 256,
+                   "fc1": 4096 + 512, "fc2": 512 + 10 + 40}
+HBM_BOUND = {"conv1"}
+
+
+def build_model(rank, device, per_channel=False):
+    from models.baseline_model import synthetic_model
+    from qconvnet import data
+    from qconvnet.dist import broadcast_object
+    from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
+    payload = None
+    if rank == 0:
+        calib = torch.from_numpy(data.synthetic_images(512, 1))
+        fp = synthetic_model(0, calib)
+        folded = fold_state_dict(fp.state_dict())
+        ranges = calibrate(folded, [calib], "cpu")
+        payload = (build_qspec(folded, ranges, "static", per_channel), fp.state_dict())
+    spec, sd = broadcast_object(payload)
+    return QuantizedConvNet(spec, device), sd
+
+
+def cpu_baselines(state_dict, qmodel_gpu, seconds):
+    """Reference CPU paths on the host cores (rank 0, N = 1 only)."""
+    from oracle import torch_ref
+    from qconvnet import data
+    fp = torch_ref.SimpleConvNetRef()
+    fp.load_state_dict(state_dict)
+    fp.eval()
+    threads = torch.get_num_threads()
+    out = {}
+    # (1) StaticPTQModel as the reference builds it (static_ptq_model.py:19-34):
+    #     quantize_dynamic({Linear, Conv2d}, qint8) -> fp32 convs + dynamic int8 fc
+    sp = torch_ref.build_static_ptq_cpu(fp)
+    bs = 32
+    x = torch.from_numpy(data.synthetic_images(bs, 11))
+    with torch.no_grad():
+        for _ in range(3):
+            sp(x)
+        total, iters = 0.0, 0
+        while total < seconds:
+            t0 = time.time()
+            sp(x)
+            total += time.time() - t0
+            iters += 1
+    out["static_ptq"] = {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
+                         "kind": "port",
+                         "sample": f"reference StaticPTQModel path (torch.ao quantize_dynamic "
+                                   f"{{Linear,Conv2d}} qint8 on our SimpleConvNet restatement), "
+                                   f"batch {bs} x {iters} iters, time.time() loop as "
+                                   f"utils/inference_benchmark.py:92-100"}
+    # (2) full static int8 on the CPU (torch.ao eager, fbgemm) — apples to apples
+    calib = torch.from_numpy(data.synthetic_images(512, 1))
+    q = torch_ref.build_static_int8_cpu(fp, [calib])
+    bs2 = 256
+    x2 = torch.from_numpy(data.synthetic_images(bs2, 12))
+    with torch.no_grad():
+        q(x2)
+        total, iters = 0.0, 0
+        while total < seconds / 2:
+            t0 = time.time()
+            q(x2)
+            total += time.time() - t0
+            iters += 1
+    out["static_int8"] = {"value": bs2 * iters / total, "unit": "images/sec", "cores": threads,
+                          "kind": "port",
+                          "sample": f"torch.ao eager static int8 (fbgemm), batch {bs2} x {iters} iters"}
+    # (3) top-1 agreement on 1024 synthetic images (labels = fp32 argmax: no CIFAR offline)
+    xe = torch.from_numpy(data.synthetic_images(1024, 13))
+    with torch.no_grad():
+        lab = fp(xe).argmax(1)
+        ref_top1 = (sp(xe).argmax(1) == lab).float().mean().item() * 100
+        gpu_top1 = (qmodel_gpu(xe).argmax(1) == lab).float().mean().item() * 100
+        cpu_int8_top1 = (q(xe).argmax(1) == lab).float().mean().item() * 100
+    out["top1"] = {"labels": "fp32 SimpleConvNet argmax on 1024 synthetic images",
+                   "gpu_int8_static": gpu_top1, "cpu_reference_static_ptq": ref_top1,
+                   "cpu_torchao_static_int8": cpu_int8_top1,
+                   "delta_vs_reference_pct": gpu_top1 - ref_top1}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--per-channel", action="store_true")
+    args = ap.parse_args()
+
+    from qconvnet import data
+    from qconvnet import dist as qd
+
+    rank, world, local = qd.init()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
+
+    model, sd = build_model(rank, dev, args.per_channel)
+    B = args.batch
+    x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
+    gathered = torch.empty((world * B, 10), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step(marks=None):
+        logits = model.run(x, marks=marks)
+        if world > 1:
+            qd.gather_logits(logits, gathered)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region A: the metric
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    images = world * B * args.steps
+    value = images / elapsed
+
+    # ---- timed region B: per-kernel HIP events (same steps, same stream)
+    marks_all = []
+    barrier()
+    torch.cuda.synchronize()
+    for _ in range(args.steps):
+        m = []
+        step(m)
+        marks_all.append(m)
+    torch.cuda.synchronize()
+    names = model.KERNELS
+    per = {n: [] for n in names}
+    for m in marks_all:
+        for i, n in enumerate(names):
+            per[n].append(m[i].elapsed_time(m[i + 1]))
+    kern = {}
+    for n in names:
+        ms = float(np.mean(per[n]))
+        ops_ = 2.0 * MAC_PER_IMAGE[n] * B
+        byts = BYTES_PER_IMAGE[n] * B
+        kern[n] = {"ms": ms, "tops": ops_ / (ms * 1e-3) / 1e12,
+                   "gbs": byts / (ms * 1e-3) / 1e9,
+                   "bound": "hbm" if n in HBM_BOUND else "mfma"}
+        kern[n]["frac"] = (kern[n]["gbs"] / PEAK_HBM_GBS if n in HBM_BOUND
+                           else kern[n]["tops"] / PEAK_INT8_TOPS)
+    dom = max(names, key=lambda n: kern[n]["ms"])
+    k = kern[dom]
+    if k["bound"] == "mfma":
+        roof = {"kernel": dom, "bound": "mfma", "achieved": k["tops"], "peak": PEAK_INT8_TOPS,
+                "unit": "TFLOP/s", "frac": k["frac"], "traffic": None,
+                "note": "int8 TOPS reported in the TFLOP/s slot; achieved = 2*MAC*1024 / mean HIP-event duration"}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": k["gbs"], "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": k["frac"], "traffic": None}
+
+    result = {
+        "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int8", "data": "synthetic",
+        "config": {"workload": "full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
+                               "NHWC, per-tensor weights" + (" [per-channel]" if args.per_channel else ""),
+                   "global_batch": world * B, "per_gpu_batch": B, "image": [3, 32, 32],
+                   "parallelism": f"dp{world}", "collective": "all_gather logits (RCCL)" if world > 1 else None},
+        "roofline": roof,
+        "kernels": {n: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in kern[n].items()}
+                    for n in names},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baselines(sd, model, args.cpu_seconds)
+        result["cpu_baseline"] = cb["static_ptq"]
+        result["cpu_static_int8"] = cb["static_int8"]
+        result["top1"] = cb["top1"]
+        result["gpu_vs_cpu_ratio"] = value / cb["static_ptq"]["value"]
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

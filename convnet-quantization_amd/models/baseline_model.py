@@ -63,6 +63,37 @@ def load_checkpoint_state(obj):
     return obj
 
 
+def recalibrate_bn(model, images):
+    """Synthetic-weight helper (random-init BN statistics make
+    the argmax degenerate): set every BatchNorm's running stats to the batch
+    statistics of ``images`` (train-mode forward, cumulative average), then
+    return the model in eval mode.  Parameters are not touched."""
+    model.train()
+    for m in model.modules():
+        if isinstance(m, nn.Dropout):
+            m.eval()
+    bns = [m for m in model.modules() if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d))]
+    saved = [m.momentum for m in bns]
+    for m in bns:
+        m.reset_running_stats()
+        m.momentum = None
+    with torch.no_grad():
+        model(images)
+    for m, mom in zip(bns, saved):
+        m.momentum = mom
+    return model.eval()
+
+
+def synthetic_model(seed=0, calib_images=None):
+    """Random-init SimpleConvNet (torch seed) with BN recalibrated on
+    ``calib_images`` — the benchmark's stand-in for trained weights."""
+    torch.manual_seed(seed)
+    model = SimpleConvNet()
+    if calib_images is not None:
+        recalibrate_bn(model, calib_images)
+    return model.eval()
+
+
 def test_model():
     model = SimpleConvNet()
     y = model(torch.randn(1, 3, 32, 32))

@@ -278,34 +278,50 @@ class QuantizedConvNet:
         return b
 
     # --------------------------------------------------------------- forward
-    def run(self, x, keep=False):
+    KERNELS = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2")
+
+    def run(self, x, keep=False, marks=None):
         """Launch the whole int8 forward on the current stream (no sync).
         Returns the fp32 logits tensor (a reused buffer); with keep=True also
-        the dict of intermediate u8 activations."""
+        the dict of intermediate u8 activations.  ``marks``: a list that
+        receives 9 timing events (before conv1, after each of the 8 kernels)."""
         n = x.shape[0]
         b = self._buffers(n)
         L = self.L
+
+        def mark():
+            if marks is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                marks.append(ev)
+
+        mark()
         d = L[0]
         ops.conv1_f32(x, self.in_scale, self.in_zp, d.w, d.u, d.v, d.mult, d.corr, d.z_y, d.relu,
                       d.qdq, out=b["a1"])
+        mark()
         prev = b["a1"]
         names = ["a2", "a3", "a4", "a5", "a6"]
         for i in range(1, 6):
             d = L[i]
             ops.conv3x3(prev, d.z_x, d.w, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, d.pool,
                         d.qdq, out=b[names[i - 1]])
+            mark()
             prev = b[names[i - 1]]
         flat = prev.view(n, 4096)
         f1, f2 = self.fc1, self.fc2
         if self.mode == "static":
             ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, True,
                           out=b["f1"])
+            mark()
             ops.linear_u8(b["f1"], f2.z_x, f2.w, f2.u, f2.v, f2.mult, f2.corr, f2.z_y, False,
                           y_scale=f2.s_y, want_fp32=True, out=b["q"], out_f=b["logits"])
         else:
             ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, False,
                           y_scale=f1.s_y, want_fp32=True, out=b["f1"], out_f=b["f1f"])
+            mark()
             ops.linear_f32(b["f1f"], f2.w, f2.b, relu_in=True, out=b["logits"])
+        mark()
         if keep:
             return b["logits"], b
         return b["logits"]
