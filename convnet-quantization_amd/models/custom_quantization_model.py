@@ -1,0 +1,91 @@
+"""CustomQuantizationModel — drop-in for
+/root/reference/models/custom_quantization_model.py:145-261 (BASELINE config 2).
+
+Reference behaviour: engine select (fbgemm, else qnnpack, else RuntimeError,
+:155-161); load_state_dict (:163-167); quantize() = eval -> cpu ->
+fuse_modules [conv_i, bn_i] x6 + [fc1, bn7] (:180-190) ->
+CustomQuantizedSimpleConvNet, where every conv and fc1 is wrapped
+QuantStub -> op -> DeQuantStub (:34-58), ReLU / max-pool run in fp32 outside the
+wrapper (:237-252) and fc2 stays fp32 (:219).  As shipped, the stubs are never
+converted, so the reference model is still fp32.
+
+Here the stubs are live: quantize() calibrates every stub (MinMax observers,
+per-tensor affine activations, symmetric s8 weights) and builds the per-layer
+QDQ int8 model on the MI355X (``QuantizedConvNet`` in "qdq" mode) — each
+conv's epilogue requantizes to its own output qparams and then performs the
+dequantize -> ReLU -> [pool] -> quantize(next stub) hand-off in registers, with
+torch.ao's fp32 op order, so the integer chain is bit-exact with torch.ao
+(fbgemm) and only the fp32 fc2 GEMM differs by summation order.
+"""
+from __future__ import annotations
+
+import torch
+
+from models.baseline_model import SimpleConvNet, load_checkpoint_state
+from qconvnet import data
+from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
+
+
+class CustomQuantizationModel:
+    def __init__(self, device="cuda"):
+        self.model = SimpleConvNet()
+        self.quantized_model = None
+        self.is_custom_quantized = True
+        self.device = device
+        # the reference selects a CPU quantization engine and raises if none
+        # exists; the MI355X path needs the HIP library instead
+        from qconvnet import _lib
+        try:
+            _lib.load()
+        except _lib.QcnError as e:
+            raise RuntimeError("No supported quantization engine found: " + str(e)) from e
+
+    def load_state_dict(self, state_dict):
+        self.model.load_state_dict(load_checkpoint_state(state_dict))
+
+    def quantize(self, calibration_data_loader=None, per_channel=False, calibration_device="cpu",
+                 max_batches=None):
+        self.model.eval()
+        folded = fold_state_dict(self.model.state_dict())
+        batches = data.calibration_batches(calibration_data_loader, max_batches)
+        ranges = calibrate(folded, batches, calibration_device)
+        spec = build_qspec(folded, ranges, "qdq", per_channel)
+        self.quantized_model = QuantizedConvNet(spec, self.device)
+        return self.quantized_model
+
+    def forward(self, x):
+        if self.quantized_model is not None:
+            return self.quantized_model(x)
+        return self.model(x)
+
+    def __call__(self, x):
+        return self.forward(x)
+
+    def eval(self):
+        self.model.eval()
+        return self
+
+    def to(self, device):
+        if self.quantized_model is not None:
+            self.quantized_model.to(device)
+        else:
+            self.model.to(device)
+        return self
+
+    def cpu(self):
+        return self.to("cpu")
+
+    def state_dict(self):
+        return self.model.state_dict()
+
+
+def test_custom_quantization():
+    model = CustomQuantizationModel()
+    x = torch.randn(1, 3, 32, 32)
+    y = model(x)
+    print(f"Input shape: {tuple(x.shape)}\nOutput shape: {tuple(y.shape)}")
+    return model
+
+
+if __name__ == "__main__":
+    test_custom_quantization()

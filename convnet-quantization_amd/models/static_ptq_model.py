@@ -22,10 +22,18 @@ from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state
 
 
 class StaticPTQModel:
-    def __init__(self, device="cuda"):
+    """mode="static" (default): full static int8 on the MI355X.
+    mode="reference": the reference's actual semantics — quantize_dynamic on the
+    unfolded net (fp32 convs + BN, dynamic int8 fc1/fc2; the dynamic Linear on
+    the HIP kernel)."""
+
+    def __init__(self, device="cuda", mode="static"):
+        if mode not in ("static", "reference"):
+            raise ValueError(f"unknown mode {mode!r}")
         self.fp32_model = SimpleConvNet()
         self.quantized_model = None
         self.device = device
+        self.mode = mode
 
     def load_state_dict(self, state_dict):
         self.fp32_model.load_state_dict(load_checkpoint_state(state_dict))
@@ -35,6 +43,11 @@ class StaticPTQModel:
         """Calibrate (fp32, BN folded — the reference quantizes on the CPU, so
         does the default here) and build the int8 GPU model."""
         self.fp32_model.eval()
+        if self.mode == "reference":
+            from models.dynamic_ptq_model import DynamicQuantConvNet
+            self.quantized_model = DynamicQuantConvNet(self.fp32_model.state_dict(), fold=False,
+                                                       device=self.device)
+            return self.quantized_model
         folded = fold_state_dict(self.fp32_model.state_dict())
         batches = data.calibration_batches(calibration_data_loader, max_batches)
         ranges = calibrate(folded, batches, calibration_device)
