@@ -27,29 +27,47 @@
 
 namespace qcn {
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX>
+// Patch layout knobs (chosen per layer by an offline bank-conflict search so
+// that every ds_read_b128 of an MFMA operand is conflict-free):
+//   PSP  bytes of padding per staged pixel (pixel stride PS = CIN + PSP)
+//   RPAD bytes of padding per staged row,  SPAD per staged image segment
+//   SPLIT store even patch columns before odd ones (pooled layers read stride-2)
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
+          int SPAD = 0, bool SPLIT = false>
 struct ConvCfg {
   static constexpr int W = HW, H = HW;
   static constexpr int WCO = COUT / 64;          // waves along cout
   static constexpr int NWAVES = WCO * WPX;
   static constexpr int NT = NWAVES * 64;         // threads
-  static constexpr int PXB = WPX * 128;          // output pixels per workgroup
+  static constexpr int PXB = WPX * 128;          // output pixels per workgroup (pre-pool)
+  static constexpr int OPX = POOL ? PXB / 4 : PXB;  // output pixels written
   static constexpr int IMG = H * W;
   static constexpr int SEGS = PXB >= IMG ? PXB / IMG : 1;
   static constexpr int R = PXB >= IMG ? H : PXB / W;   // rows per segment
-  static constexpr int PS = CIN + 16;            // LDS bytes per staged pixel
+  static constexpr int PS = CIN + PSP;
   static constexpr int PROWS = R + 2, PCOLS = W + 2;
-  static constexpr int PATCH = SEGS * PROWS * PCOLS * PS;
-  static constexpr int WS = 64 + 16;             // LDS bytes per cout per chunk
-  static constexpr int WBUF = COUT * WS;
+  static constexpr int HALF = (PCOLS + 1) / 2;
+  static constexpr int RS = PCOLS * PS + RPAD;
+  static constexpr int SS = PROWS * RS + SPAD;
+  static constexpr int PATCH = SEGS * SS;
+  static constexpr int WBUF = COUT * 64;         // one K-chunk of weights (XOR-swizzled rows)
+  static constexpr int NG = WBUF / (NWAVES * 1024);  // global_load_lds per wave per chunk
   static constexpr int NCH = 9 * CIN / 64;       // K chunks
-  static constexpr int LDS = PATCH + 2 * WBUF;
-  static constexpr int WLOADS = COUT * 4 / NT;   // 16-B weight loads per thread per chunk
+  static constexpr int OS = COUT + 16;           // output staging row stride
+  static constexpr int MAIN = PATCH + 3 * WBUF;  // patch + 3-deep weight ring
+  static constexpr int OUT = OPX * OS;
+  static constexpr int LDS = MAIN > OUT ? MAIN : OUT;
   static_assert(CIN % 64 == 0 && COUT % 64 == 0, "channel multiples of 64");
+  static_assert(PSP % 16 == 0 && RPAD % 16 == 0 && SPAD % 16 == 0, "16-B aligned layout");
   static_assert(PXB % W == 0, "workgroup covers whole rows");
   static_assert(PXB >= IMG ? (PXB % IMG == 0) : (H % R == 0), "rows tile the image");
   static_assert(!POOL || (R % 2 == 0), "pooled rows come in pairs");
-  static_assert(COUT * 4 % NT == 0 && WLOADS >= 1, "weight staging split");
+  static_assert(NG >= 1 && WBUF % (NWAVES * 1024) == 0, "weight ring split");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  __device__ static constexpr int slot(int seg, int prow, int pcol) {
+    const int cpos = SPLIT ? ((pcol & 1) * HALF + (pcol >> 1)) : pcol;
+    return seg * SS + prow * RS + cpos * PS;
+  }
 };
 
 struct ConvEpi {
@@ -62,15 +80,70 @@ struct ConvEpi {
   float s1; int z1; float inv2; int z2;
 };
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX>
-__global__ __launch_bounds__(COUT * WPX)
+// Requantize one 32(cout) x 32(pixel) accumulator tile (optionally the max of
+// four quadrant tiles) and write it to the LDS output image [pixel][cout]:
+// two rounds of v_permlane32_swap turn the MFMA layout (4 couts per register,
+// lane halves interleaved every 4 couts) into 16 contiguous couts per lane,
+// so each lane issues ONE conflict-free ds_write_b128.
+template <int NQ>
+QCN_DEV void epilogue_tile(const v16i* accs, const ConvEpi& ep, int co_base, int hi,
+                           uint8_t* orow) {
+  uint32_t w[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int co = co_base + 8 * g + 4 * hi;
+    const float4 u4 = *reinterpret_cast<const float4*>(ep.u + co);
+    const float4 v4 = *reinterpret_cast<const float4*>(ep.v + co);
+    const float4 m4 = *reinterpret_cast<const float4*>(ep.mult + co);
+    const int4 c4 = *reinterpret_cast<const int4*>(ep.corr + co);
+    const float uu[4] = {u4.x, u4.y, u4.z, u4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    const float mm[4] = {m4.x, m4.y, m4.z, m4.w};
+    const int cc[4] = {c4.x, c4.y, c4.z, c4.w};
+    uint32_t wd = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rg = 4 * g + e;
+      int a = accs[0][rg];
+      if constexpr (NQ == 4) a = max(max(a, accs[1][rg]), max(accs[2][rg], accs[3][rg]));
+      int q = requant_one(a + cc[e], uu[e], vv[e], mm[e], ep.zp_y, ep.lo);
+      if (ep.qdq) q = qdq_next(q, ep.s1, ep.z1, ep.inv2, ep.z2);
+      wd |= (uint32_t)q << (8 * e);
+    }
+    w[g] = wd;
+  }
+  // low lanes: c0-3 | c8-11 | c16-19 | c24-27 ; high lanes: c4-7 | c12-15 | ...
+  auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
+  auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
+  w[0] = s01[0]; w[1] = s01[1]; w[2] = s23[0]; w[3] = s23[1];
+  auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+  auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+  w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
+  // now low lanes hold couts co_base + 0..15, high lanes co_base + 16..31
+  *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Copy the staged [opx][cout] u8 tile (row stride OS) to its contiguous NHWC
+// destination with 16-B coalesced stores (full cache lines, no partial writes).
+template <int COUT, int OS, int NT>
+QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid) {
+  constexpr int CPR = COUT / 16;
+  const int total = opx * CPR;
+  for (int e = tid; e < total; e += NT) {
+    const int row = e / CPR, ch = e % CPR;
+    if (row < valid_px)
+      *reinterpret_cast<uint4*>(dst + (long)row * COUT + ch * 16) =
+          *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16);
+  }
+}
+
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
+__global__ __launch_bounds__(COUT * WPX, 2)
 void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                          const int8_t* __restrict__ wpk, ConvEpi ep,
                          uint8_t* __restrict__ y) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX>;
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* patch = lds;
-  uint8_t* wbuf0 = lds + C::PATCH;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -80,7 +153,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int l32 = lane & 31;
   const int hi = lane >> 5;
 
-  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel
+  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
   const int n0 = (int)(p0 / C::IMG);
   const int y0 = (int)((p0 % C::IMG) / C::W);
 
@@ -89,9 +162,9 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   constexpr int CH16 = CIN / 16;
   constexpr int NSLOT = C::SEGS * C::PROWS * C::PCOLS;
   for (int it = tid; it < NSLOT * CH16; it += C::NT) {
-    const int slot = it / CH16, chunk = it % CH16;
-    const int seg = slot / (C::PROWS * C::PCOLS);
-    const int rem = slot % (C::PROWS * C::PCOLS);
+    const int sl = it / CH16, chunk = it % CH16;
+    const int seg = sl / (C::PROWS * C::PCOLS);
+    const int rem = sl % (C::PROWS * C::PCOLS);
     const int pr = rem / C::PCOLS, pc = rem % C::PCOLS;
     const int n = n0 + seg, yy = y0 + pr - 1, xx = pc - 1;
     uint4 val = make_uint4(padw, padw, padw, padw);
@@ -100,41 +173,49 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
           x + (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16);
       val = make_uint4(xor80(g.x), xor80(g.y), xor80(g.z), xor80(g.w));
     }
-    *reinterpret_cast<uint4*>(patch + slot * C::PS + chunk * 16) = val;
+    *reinterpret_cast<uint4*>(patch + C::slot(seg, pr, pc) + chunk * 16) = val;
   }
 
-  // ---- stage weight chunk 0
-  auto wsrc = [&](int ch, int i) {
-    const int e = tid + i * C::NT;          // 16-byte element within the chunk
-    return reinterpret_cast<const uint4*>(wpk + (long)ch * COUT * 64) + e;
-  };
-  auto wdst = [&](uint8_t* buf, int i) {
-    const int e = tid + i * C::NT;
-    return reinterpret_cast<uint4*>(buf + (e >> 2) * C::WS + (e & 3) * 16);
-  };
+  // ---- weight ring: K-chunk ch (64 input channels of one tap, all COUT rows
+  // of 64 B) -> buffer ch % 3 by LDS-DMA (global_load_lds, 16 B per lane),
+  // two chunks in flight.  Row r's 16-B slot c is stored at slot c ^ ((r>>2)&3)
+  // (swizzle applied on the SOURCE address, the LDS image stays lane-linear)
+  // so the A-operand ds_read_b128 of 16 consecutive rows is conflict-free.
+  uint8_t* wring = lds + C::PATCH;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](int ch) {
+    uint8_t* buf = wring + (ch % 3) * C::WBUF;
+    const int8_t* base = wpk + (long)ch * C::WBUF;
 #pragma unroll
-  for (int i = 0; i < C::WLOADS; ++i) *wdst(wbuf0, i) = *wsrc(0, i);
+    for (int g = 0; g < C::NG; ++g) {
+      const int o = (g * C::NWAVES + wave_u) * 1024 + lane * 16;
+      const int r = o >> 6, sl = (o >> 4) & 3;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4)),
+          (void*)(buf + (g * C::NWAVES + wave_u) * 1024), 16, 0, 0);
+    }
+  };
 
-  // ---- per-lane pixel slots of the four pixel tiles
-  int pslot[4];
+  // ---- per-lane patch positions of the four pixel tiles (tap (0,0), channel 0)
+  int pseg[4], prow[4], pcol[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    int seg, yy, xx;
     if constexpr (POOL) {
       constexpr int PW = C::W / 2, PR = C::R / 2;
       const int q = wp * 32 + l32;
-      seg = q / (PR * PW);
-      yy = 2 * ((q / PW) % PR) + (j >> 1);
-      xx = 2 * (q % PW) + (j & 1);
+      pseg[j] = q / (PR * PW);
+      prow[j] = 2 * ((q / PW) % PR) + (j >> 1);
+      pcol[j] = 2 * (q % PW) + (j & 1);
     } else {
       const int m = (wp * 4 + j) * 32 + l32;
-      seg = m / (C::R * C::W);
-      yy = (m / C::W) % C::R;
-      xx = m % C::W;
+      pseg[j] = m / (C::R * C::W);
+      prow[j] = (m / C::W) % C::R;
+      pcol[j] = m % C::W;
     }
-    pslot[j] = ((seg * C::PROWS + yy) * C::PCOLS + xx) * C::PS + hi * 16;
   }
-  const int wrow0 = (wc * 64 + l32) * C::WS + hi * 16;
+  // A operand: row wc*64 + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
+  const int arow = wc * 64 + l32;
+  const int aswz = (arow >> 2) & 3;  // same for arow + 32
 
   v16i acc[2][4];
 #pragma unroll
@@ -142,89 +223,70 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (v16i){0};
 
-  __syncthreads();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch loads retired
+  issue(0);
+  if (C::NCH > 1) issue(1);
+  if (C::NCH > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
-  uint4 pre[C::WLOADS];
-  for (int ch = 0; ch < C::NCH; ++ch) {
-    const bool more = ch + 1 < C::NCH;
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < C::WLOADS; ++i) pre[i] = *wsrc(ch + 1, i);
-    }
-    const uint8_t* wb = wbuf0 + (ch & 1) * C::WBUF;
-    const int tap = ch / (CIN / 64);
-    const int cb = ch % (CIN / 64);
+#pragma unroll 1
+  for (int tap = 0; tap < 9; ++tap) {
     const int r = tap / 3, s = tap % 3;
-    const int poff = (r * C::PCOLS + s) * C::PS + cb * 64;
+    int paddr[4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v4i a[2], b[4];
+    for (int j = 0; j < 4; ++j) paddr[j] = C::slot(pseg[j], prow[j] + r, pcol[j] + s) + hi * 16;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        a[i] = *reinterpret_cast<const v4i*>(wb + wrow0 + i * 32 * C::WS + kk * 32);
+    for (int cb = 0; cb < CIN / 64; ++cb) {
+      const int ch = tap * (CIN / 64) + cb;
+      const bool more = ch + 2 < C::NCH;
+      if (more) issue(ch + 2);
+      const uint8_t* wb = wring + (ch % 3) * C::WBUF + arow * 64;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        b[j] = *reinterpret_cast<const v4i*>(patch + pslot[j] + poff + kk * 32);
+      for (int kk = 0; kk < 2; ++kk) {
+        v4i a[2], b[4];
+        const int aoff = ((2 * kk + hi) ^ aswz) << 4;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
+          a[i] = *reinterpret_cast<const v4i*>(wb + i * 32 * 64 + aoff);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      uint8_t* nb = wbuf0 + ((ch + 1) & 1) * C::WBUF;
+          b[j] = *reinterpret_cast<const v4i*>(patch + paddr[j] + cb * 64 + kk * 32);
 #pragma unroll
-      for (int i = 0; i < C::WLOADS; ++i) *wdst(nb, i) = pre[i];
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      // chunk ch+1 must have landed before the barrier that precedes its reads
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
-    __syncthreads();
   }
 
-  // ---- epilogue
-  // accumulator element (reg rg) of tile (i, j): cout row = 32i + (rg&3) + 8(rg>>2) + 4hi,
-  // pixel column = l32 of pixel tile j.
-  const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
+  // ---- epilogue: requant in registers -> LDS [pixel][cout] -> coalesced stores
+  uint8_t* lout = lds;  // the patch / weight ring is dead after the last barrier
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    int res[4][16];
-    constexpr int NJ = POOL ? 1 : 4;
+    const int co_base = wc * 64 + i * 32;
+    if constexpr (POOL) {
+      const int opx = wp * 32 + l32;
+      epilogue_tile<4>(acc[i], ep, co_base, hi, lout + opx * C::OS);
+    } else {
 #pragma unroll
-    for (int rg = 0; rg < 16; ++rg) {
-      const int co = wc * 64 + i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hi;
-      const int corr = ep.corr[co];
-      const float u = ep.u[co], v = ep.v[co], mu = ep.mult[co];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        int a;
-        if constexpr (POOL) {
-          a = max(max(acc[i][0][rg], acc[i][1][rg]), max(acc[i][2][rg], acc[i][3][rg]));
-        } else {
-          a = acc[i][j][rg];
-        }
-        int q = requant_one(a + corr, u, v, mu, ep.zp_y, ep.lo);
-        if (ep.qdq) q = qdq_next(q, ep.s1, ep.z1, ep.inv2, ep.z2);
-        res[j][rg] = q;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      long opix;
-      if constexpr (POOL) {
-        opix = (long)blockIdx.x * (C::PXB / 4) + wp * 32 + l32;
-      } else {
-        opix = p0 + (wp * 4 + j) * 32 + l32;
-      }
-      if (opix < total_out) {
-        uint8_t* dst = y + opix * COUT + wc * 64 + i * 32 + 4 * hi;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t w32 = (uint32_t)res[j][4 * g] | ((uint32_t)res[j][4 * g + 1] << 8) |
-                               ((uint32_t)res[j][4 * g + 2] << 16) |
-                               ((uint32_t)res[j][4 * g + 3] << 24);
-          *reinterpret_cast<uint32_t*>(dst + 8 * g) = w32;
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int opx = (wp * 4 + j) * 32 + l32;
+        epilogue_tile<1>(&acc[i][j], ep, co_base, hi, lout + opx * C::OS);
       }
     }
   }
+  __syncthreads();
+  const long out0 = (long)blockIdx.x * C::OPX;
+  const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
+  store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
 }
 
 // --------------------------------------------------------------------------
@@ -243,7 +305,7 @@ struct Conv1Cfg {
 };
 
 template <int HW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(256, 3)
 void conv1_f32_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
                       const int8_t* __restrict__ w1, ConvEpi ep, uint8_t* __restrict__ y,
                       uint8_t* __restrict__ qin_out) {
@@ -324,31 +386,16 @@ void conv1_f32_kernel(const float* __restrict__ x, int nimg, float in_inv, int i
     for (int i = 0; i < 2; ++i)
       acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b, (v16i){0}, 0, 0, 0);
   }
+  __syncthreads();  // im2col / patch are dead: the LDS becomes the output image
+  uint8_t* lout = lds;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epilogue_tile<1>(&acc[i][j], ep, i * 32, hi, lout + ((wave * 4 + j) * 32 + l32) * 80);
+  __syncthreads();
   const long total = (long)nimg * H * W;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long opix = p0 + (wave * 4 + j) * 32 + l32;
-      int res[16];
-#pragma unroll
-      for (int rg = 0; rg < 16; ++rg) {
-        const int co = i * 32 + (rg & 3) + 8 * (rg >> 2) + 4 * hi;
-        int q = requant_one(acc[i][j][rg] + ep.corr[co], ep.u[co], ep.v[co], ep.mult[co],
-                            ep.zp_y, ep.lo);
-        if (ep.qdq) q = qdq_next(q, ep.s1, ep.z1, ep.inv2, ep.z2);
-        res[rg] = q;
-      }
-      if (opix < total) {
-        uint8_t* dst = y + opix * 64 + i * 32 + 4 * hi;
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint32_t*>(dst + 8 * g) =
-              (uint32_t)res[4 * g] | ((uint32_t)res[4 * g + 1] << 8) |
-              ((uint32_t)res[4 * g + 2] << 16) | ((uint32_t)res[4 * g + 3] << 24);
-      }
-    }
-  }
+  store_staged<64, 80, 256>(lout, 512, y + p0 * 64, total - p0, tid);
 }
 
 // --------------------------------------------------------------------------
@@ -402,13 +449,14 @@ __global__ void conv3x3_generic_kernel(const uint8_t* __restrict__ x, int nimg, 
 namespace {
 using namespace qcn;
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX>
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
+          int SPAD = 0, bool SPLIT = false>
 int launch_conv(const uint8_t* x, int nimg, int x_zp, const int8_t* wpk, const ConvEpi& ep,
                 uint8_t* y, hipStream_t st) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX>;
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
   const long pix = (long)nimg * C::IMG;
   const int grid = (int)((pix + C::PXB - 1) / C::PXB);
-  auto k = conv3x3_u8s8_kernel<CIN, COUT, HW, POOL, WPX>;
+  auto k = conv3x3_u8s8_kernel<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
   static bool attr_done = false;
   if (!attr_done) {
     if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
@@ -424,25 +472,26 @@ int launch_conv(const uint8_t* x, int nimg, int x_zp, const int8_t* wpk, const C
 // small shapes the parity fixtures use.
 int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nimg, int x_zp,
                   const int8_t* wpk, const ConvEpi& ep, uint8_t* y, hipStream_t st) {
-#define QCN_CONV_CASE(CI, CO, HWV, PL, WPXV)                                          \
+#define QCN_CONV_CASE(CI, CO, HWV, PL, WPXV, ...)                                      \
   if (cin == CI && cout == CO && hw == HWV && pool == PL)                              \
-    return launch_conv<CI, CO, HWV, PL, WPXV>(x, nimg, x_zp, wpk, ep, y, st);
-  QCN_CONV_CASE(64, 64, 32, 1, 4)
-  QCN_CONV_CASE(64, 64, 32, 0, 4)
-  QCN_CONV_CASE(64, 128, 16, 0, 2)
-  QCN_CONV_CASE(128, 128, 16, 1, 2)
-  QCN_CONV_CASE(128, 128, 16, 0, 2)
-  QCN_CONV_CASE(128, 256, 8, 0, 2)
-  QCN_CONV_CASE(256, 256, 8, 1, 2)
-  QCN_CONV_CASE(256, 256, 8, 0, 2)
-  QCN_CONV_CASE(64, 64, 16, 0, 2)
-  QCN_CONV_CASE(64, 64, 16, 1, 2)
-  QCN_CONV_CASE(64, 64, 8, 0, 1)
-  QCN_CONV_CASE(64, 64, 8, 1, 2)
-  QCN_CONV_CASE(64, 128, 8, 0, 1)
-  QCN_CONV_CASE(128, 256, 4, 0, 2)
-  QCN_CONV_CASE(256, 256, 4, 0, 1)
-  QCN_CONV_CASE(256, 256, 4, 1, 1)
+    return launch_conv<CI, CO, HWV, PL, WPXV, ##__VA_ARGS__>(x, nimg, x_zp, wpk, ep, y, st);
+  //            cin  cout hw pool wpx | PSP RPAD SPAD SPLIT (bank-conflict-free layouts)
+  QCN_CONV_CASE(64, 64, 32, 1, 4, 16, 96, 0, true)
+  QCN_CONV_CASE(64, 64, 32, 0, 4, 16, 0, 0, false)
+  QCN_CONV_CASE(64, 128, 16, 0, 2, 16, 96, 0, false)
+  QCN_CONV_CASE(128, 128, 16, 1, 2, 16, 32, 0, true)
+  QCN_CONV_CASE(128, 128, 16, 0, 2, 16, 32, 0, false)
+  QCN_CONV_CASE(128, 256, 8, 0, 2, 16, 224, 0, false)
+  QCN_CONV_CASE(256, 256, 8, 1, 2, 16, 32, 64, true)
+  QCN_CONV_CASE(256, 256, 8, 0, 2, 16, 32, 64, false)
+  QCN_CONV_CASE(64, 64, 16, 0, 2, 16, 96, 0, false)
+  QCN_CONV_CASE(64, 64, 16, 1, 2, 16, 96, 0, true)
+  QCN_CONV_CASE(64, 64, 8, 0, 1, 16, 96, 0, false)
+  QCN_CONV_CASE(64, 64, 8, 1, 2, 16, 96, 0, true)
+  QCN_CONV_CASE(64, 128, 8, 0, 1, 16, 96, 0, false)
+  QCN_CONV_CASE(128, 256, 4, 0, 2, 16, 32, 64, false)
+  QCN_CONV_CASE(256, 256, 4, 0, 1, 16, 32, 64, false)
+  QCN_CONV_CASE(256, 256, 4, 1, 1, 16, 0, 0, false)
 #undef QCN_CONV_CASE
   return QCN_ERR_UNSUPPORTED;
 }
@@ -542,7 +591,8 @@ int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_
   if (hw == HWV) {                                                                        \
     constexpr int R = (HWV * HWV >= 512) ? 512 / HWV : HWV;                              \
     constexpr int SEGS = (HWV * HWV >= 512) ? 1 : 512 / (HWV * HWV);                     \
-    constexpr int LDS = ((SEGS * 3 * (R + 2) * (HWV + 2) + 15) / 16 * 16) + 512 * 48;     \
+    constexpr int LDS0 = ((SEGS * 3 * (R + 2) * (HWV + 2) + 15) / 16 * 16) + 512 * 48;    \
+    constexpr int LDS = LDS0 > 512 * 80 ? LDS0 : 512 * 80;                                \
     hipLaunchKernelGGL(qcn::conv1_f32_kernel<HWV>, dim3(grid), dim3(256), LDS, st, x, nimg, \
                        inv, in_zp, w1_packed, ep, y, q_in);                              \
     return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;                       \
