@@ -46,6 +46,25 @@ QCN_DEV int qdq_next(int q, float s1, int z1, float inv2, int z2) {
   return r;
 }
 
+// Float form of requant_one for the MFMA epilogues: returns the requantized
+// value as an integral float in [lo, 255].  rint(ab) + zp is exact while
+// |ab| < 2^24; beyond that the sum keeps its sign and the clamp saturates to
+// the same bound, so no separate range clamp is needed.  7 VALU per element
+// (cvt, fma, mul, rndne, add, med3 + the pack) instead of ~15.
+QCN_DEV float requant_f(int acc, float u, float v, float mult, float zpf, float lof) {
+  const float t = __builtin_fmaf(u, v, (float)acc);
+  const float ab = t * mult;
+  return __builtin_amdgcn_fmed3f(__builtin_rintf(ab) + zpf, lof, 255.0f);
+}
+
+// qdq_next on the float form (q integral in [0,255]): (q - z1) is exact in fp32.
+QCN_DEV float qdq_next_f(float q, float s1, float z1f, float inv2, float z2f) {
+  float x = (q - z1f) * s1;
+  x = x > 0.0f ? x : 0.0f;
+  const float t = fminf(x * inv2, 1.0e9f);
+  return __builtin_amdgcn_fmed3f(__builtin_rintf(t) + z2f, 0.0f, 255.0f);
+}
+
 QCN_DEV uint32_t xor80(uint32_t v) { return v ^ 0x80808080u; }
 
 QCN_DEV uint32_t splat_u8(int b) {

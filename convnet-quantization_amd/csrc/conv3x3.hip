@@ -35,6 +35,8 @@ namespace qcn {
 template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
           int SPAD = 0, bool SPLIT = false>
 struct ConvCfg {
+  static constexpr int kCin = CIN, kCout = COUT;
+  static constexpr bool kPool = POOL;
   static constexpr int W = HW, H = HW;
   static constexpr int WCO = COUT / 64;          // waves along cout
   static constexpr int NWAVES = WCO * WPX;
@@ -85,29 +87,44 @@ struct ConvEpi {
 // two rounds of v_permlane32_swap turn the MFMA layout (4 couts per register,
 // lane halves interleaved every 4 couts) into 16 contiguous couts per lane,
 // so each lane issues ONE conflict-free ds_write_b128.
-template <int NQ>
-QCN_DEV void epilogue_tile(const v16i* accs, const ConvEpi& ep, int co_base, int hi,
-                           uint8_t* orow) {
-  uint32_t w[4];
+// fp32 epilogue constants of the 16 output channels a lane owns in one
+// 32-channel accumulator tile (channels co_base + 8g + 4hi + e).
+struct EpiK {
+  float u[16], v[16], m[16];
+};
+QCN_DEV EpiK load_epik(const ConvEpi& ep, int co_base, int hi) {
+  EpiK k;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int co = co_base + 8 * g + 4 * hi;
     const float4 u4 = *reinterpret_cast<const float4*>(ep.u + co);
     const float4 v4 = *reinterpret_cast<const float4*>(ep.v + co);
     const float4 m4 = *reinterpret_cast<const float4*>(ep.mult + co);
-    const int4 c4 = *reinterpret_cast<const int4*>(ep.corr + co);
-    const float uu[4] = {u4.x, u4.y, u4.z, u4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
-    const float mm[4] = {m4.x, m4.y, m4.z, m4.w};
-    const int cc[4] = {c4.x, c4.y, c4.z, c4.w};
+    k.u[4 * g] = u4.x; k.u[4 * g + 1] = u4.y; k.u[4 * g + 2] = u4.z; k.u[4 * g + 3] = u4.w;
+    k.v[4 * g] = v4.x; k.v[4 * g + 1] = v4.y; k.v[4 * g + 2] = v4.z; k.v[4 * g + 3] = v4.w;
+    k.m[4 * g] = m4.x; k.m[4 * g + 1] = m4.y; k.m[4 * g + 2] = m4.z; k.m[4 * g + 3] = m4.w;
+  }
+  return k;
+}
+
+template <int NQ, bool XORIN = false>
+QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
+                             int hi, uint8_t* orow) {
+  // accumulators already include the zero-point correction (acc_init_corr)
+  uint32_t w[4];
+  const float zpf = (float)ep.zp_y, lof = (float)ep.lo;
+  const float z1f = (float)ep.z1, z2f = (float)ep.z2;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
     uint32_t wd = 0;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int rg = 4 * g + e;
       int a = accs[0][rg];
       if constexpr (NQ == 4) a = max(max(a, accs[1][rg]), max(accs[2][rg], accs[3][rg]));
-      int q = requant_one(a + cc[e], uu[e], vv[e], mm[e], ep.zp_y, ep.lo);
-      if (ep.qdq) q = qdq_next(q, ep.s1, ep.z1, ep.inv2, ep.z2);
-      wd |= (uint32_t)q << (8 * e);
+      float q = requant_f(a, K.u[rg], K.v[rg], K.m[rg], zpf, lof);
+      if (ep.qdq) q = qdq_next_f(q, ep.s1, z1f, ep.inv2, z2f);
+      wd = __builtin_amdgcn_cvt_pk_u8_f32(q, e, wd);
     }
     w[g] = wd;
   }
@@ -119,7 +136,33 @@ QCN_DEV void epilogue_tile(const v16i* accs, const ConvEpi& ep, int co_base, int
   auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
   w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
   // now low lanes hold couts co_base + 0..15, high lanes co_base + 16..31
+  if constexpr (XORIN) {  // destination is a conv input patch: store q - 128
+#pragma unroll
+    for (int g = 0; g < 4; ++g) w[g] = xor80(w[g]);
+  }
   *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int NQ, bool XORIN = false>
+QCN_DEV void epilogue_tile(const v16i* accs, const ConvEpi& ep, int co_base, int hi,
+                           uint8_t* orow) {
+  epilogue_tile_k<NQ, XORIN>(accs, load_epik(ep, co_base, hi), ep, co_base, hi, orow);
+}
+
+// Accumulator tile initialised with the zero-point correction
+// corr[co] = (128 - zp_x) * sum_k w[co][k] of its 16 output channels, so the
+// MFMA sum is the exact sum_k (q_x - zp_x) * w directly.
+QCN_DEV v16i acc_init_corr(const int* __restrict__ corr, int co_base, int hi) {
+  v16i a;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int4 c4 = *reinterpret_cast<const int4*>(corr + co_base + 8 * g + 4 * hi);
+    a[4 * g + 0] = c4.x;
+    a[4 * g + 1] = c4.y;
+    a[4 * g + 2] = c4.z;
+    a[4 * g + 3] = c4.w;
+  }
+  return a;
 }
 
 // Copy the staged [opx][cout] u8 tile (row stride OS) to its contiguous NHWC
@@ -136,52 +179,23 @@ QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long va
   }
 }
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
-__global__ __launch_bounds__(COUT * WPX, 2)
-void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                         const int8_t* __restrict__ wpk, ConvEpi ep,
-                         uint8_t* __restrict__ y) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* patch = lds;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wc = wave % C::WCO;      // cout group of this wave
-  const int wp = wave / C::WCO;      // pixel group of this wave
-  const int l32 = lane & 31;
-  const int hi = lane >> 5;
-
-  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
-  const int n0 = (int)(p0 / C::IMG);
-  const int y0 = (int)((p0 % C::IMG) / C::W);
-
-  // ---- stage the input patch (q ^ 0x80 = q - 128 as s8; halo = zp ^ 0x80)
-  const uint32_t padw = xor80(splat_u8(x_zp));
-  constexpr int CH16 = CIN / 16;
-  constexpr int NSLOT = C::SEGS * C::PROWS * C::PCOLS;
-  for (int it = tid; it < NSLOT * CH16; it += C::NT) {
-    const int sl = it / CH16, chunk = it % CH16;
-    const int seg = sl / (C::PROWS * C::PCOLS);
-    const int rem = sl % (C::PROWS * C::PCOLS);
-    const int pr = rem / C::PCOLS, pc = rem % C::PCOLS;
-    const int n = n0 + seg, yy = y0 + pr - 1, xx = pc - 1;
-    uint4 val = make_uint4(padw, padw, padw, padw);
-    if (n < nimg && yy >= 0 && yy < C::H && xx >= 0 && xx < C::W) {
-      const uint4 g = *reinterpret_cast<const uint4*>(
-          x + (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16);
-      val = make_uint4(xor80(g.x), xor80(g.y), xor80(g.z), xor80(g.w));
-    }
-    *reinterpret_cast<uint4*>(patch + C::slot(seg, pr, pc) + chunk * 16) = val;
-  }
-
-  // ---- weight ring: K-chunk ch (64 input channels of one tap, all COUT rows
+// Main MFMA loop over the 9 taps x CIN/64 K-chunks for a patch already staged
+// in LDS (q - 128 bytes, layout C::slot).  Weights stream through a 3-deep
+// LDS-DMA ring at wring.  Entered with all waves' patch writes issued (the
+// caller's loads may still be in flight); returns with the ring drained and all
+// waves past a barrier.
+template <class C>
+QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* __restrict__ wpk,
+                           const int* __restrict__ corr, int wave, int lane, v16i (&acc)[2][4]) {
+  constexpr int CIN = C::kCin;
+  constexpr bool POOL = C::kPool;
+  const int wc = wave % C::WCO, wp = wave / C::WCO;
+  const int l32 = lane & 31, hi = lane >> 5;
+  // weight ring: K-chunk ch (64 input channels of one tap, all COUT rows
   // of 64 B) -> buffer ch % 3 by LDS-DMA (global_load_lds, 16 B per lane),
   // two chunks in flight.  Row r's 16-B slot c is stored at slot c ^ ((r>>2)&3)
   // (swizzle applied on the SOURCE address, the LDS image stays lane-linear)
   // so the A-operand ds_read_b128 of 16 consecutive rows is conflict-free.
-  uint8_t* wring = lds + C::PATCH;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto issue = [&](int ch) {
     uint8_t* buf = wring + (ch % 3) * C::WBUF;
@@ -217,13 +231,14 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int arow = wc * 64 + l32;
   const int aswz = (arow >> 2) & 3;  // same for arow + 32
 
-  v16i acc[2][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const v16i c0 = acc_init_corr(corr, wc * 64 + i * 32, hi);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v16i){0};
+    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
+  }
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch loads retired
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch + corr loads retired
   issue(0);
   if (C::NCH > 1) issue(1);
   if (C::NCH > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
@@ -267,7 +282,17 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
     }
   }
 
-  // ---- epilogue: requant in registers -> LDS [pixel][cout] -> coalesced stores
+}
+
+// Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
+// the workgroup's contiguous NHWC output span with 16-B stores.
+template <class C>
+QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, int nimg,
+                           int wave, int lane, int tid, uint8_t* __restrict__ y) {
+  const int wc = wave % C::WCO, wp = wave / C::WCO;
+  const int l32 = lane & 31, hi = lane >> 5;
+  constexpr bool POOL = C::kPool;
+  constexpr int COUT = C::kCout;
   uint8_t* lout = lds;  // the patch / weight ring is dead after the last barrier
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -287,6 +312,64 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const long out0 = (long)blockIdx.x * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
   store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
+}
+
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
+__global__ __launch_bounds__(COUT * WPX, 2)
+void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                         const int8_t* __restrict__ wpk, ConvEpi ep,
+                         uint8_t* __restrict__ y) {
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* patch = lds;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
+  const int n0 = (int)(p0 / C::IMG);
+  const int y0 = (int)((p0 % C::IMG) / C::W);
+
+  // ---- stage the input patch (q ^ 0x80 = q - 128 as s8; halo = zp ^ 0x80).
+  // Loads are issued in unconditional batches (halo / tail lanes read a valid
+  // dummy address and are replaced afterwards) so a thread keeps BATCH 16-B
+  // loads in flight instead of one dependent HBM round trip per element.
+  const uint32_t padw = xor80(splat_u8(x_zp));
+  constexpr int CH16 = CIN / 16;
+  constexpr int NSLOT = C::SEGS * C::PROWS * C::PCOLS;
+  constexpr int TOTAL = NSLOT * CH16;
+  constexpr int NITER = (TOTAL + C::NT - 1) / C::NT;
+  constexpr int BATCH = NITER < 8 ? NITER : 8;
+  for (int b0 = 0; b0 < NITER; b0 += BATCH) {
+    uint4 v[BATCH];
+    int dst[BATCH];
+    bool inside[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int it = tid + (b0 + k) * C::NT;
+      const int itc = it < TOTAL ? it : 0;
+      const int sl = itc / CH16, chunk = itc % CH16;
+      const int seg = sl / (C::PROWS * C::PCOLS);
+      const int rem = sl % (C::PROWS * C::PCOLS);
+      const int pr = rem / C::PCOLS, pc = rem % C::PCOLS;
+      const int n = n0 + seg, yy = y0 + pr - 1, xx = pc - 1;
+      inside[k] = n < nimg && yy >= 0 && yy < C::H && xx >= 0 && xx < C::W;
+      dst[k] = (it < TOTAL && b0 + k < NITER) ? C::slot(seg, pr, pc) + chunk * 16 : -1;
+      const long src = inside[k] ? (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16 : 0;
+      v[k] = *reinterpret_cast<const uint4*>(x + src);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const uint4 val = inside[k] ? make_uint4(xor80(v[k].x), xor80(v[k].y), xor80(v[k].z), xor80(v[k].w))
+                                  : make_uint4(padw, padw, padw, padw);
+      if (dst[k] >= 0) *reinterpret_cast<uint4*>(patch + dst[k]) = val;
+    }
+  }
+
+  v16i acc[2][4];
+  conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
+  conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
 }
 
 // --------------------------------------------------------------------------
@@ -384,7 +467,8 @@ void conv1_f32_kernel(const float* __restrict__ x, int nimg, float in_inv, int i
     const v4i b = *reinterpret_cast<const v4i*>(cols + m * KS + hi * 16);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b, (v16i){0}, 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b, acc_init_corr(ep.corr, i * 32, hi),
+                                                        0, 0, 0);
   }
   __syncthreads();  // im2col / patch are dead: the LDS becomes the output image
   uint8_t* lout = lds;
@@ -396,6 +480,135 @@ void conv1_f32_kernel(const float* __restrict__ x, int nimg, float in_inv, int i
   __syncthreads();
   const long total = (long)nimg * H * W;
   store_staged<64, 80, 256>(lout, 512, y + p0 * 64, total - p0, tid);
+}
+
+// --------------------------------------------------------------------------
+// conv1 + conv2 fused (SimpleConvNet block 1: QuantStub -> conv1+ReLU ->
+// conv2+ReLU -> 2x2 max-pool).  conv1's 64-channel output never reaches HBM:
+// each workgroup (16 output rows of one 32x32 image, 4 waves) recomputes conv1
+// for the 18 x 32 positions conv2's 3x3 window needs (1.125x conv1 work, which
+// is 4.7 % of conv2's) straight into conv2's LDS input patch, then runs the
+// shared conv2 main loop.  Saves the 64 MB write + 64 MB read of the
+// activation at batch 1024.  Numerics are those of the unfused pair.
+using Conv2Cfg = ConvCfg<64, 64, 32, true, 4, 16, 96, 0, true>;
+struct Conv12 {
+  static constexpr int IN_R = 20, IN_C = 36;                 // fp32 input window
+  static constexpr int IN8 = IN_R * IN_C * 3;                 // s8 [row][col][c]
+  static constexpr int IN8_AL = (IN8 + 4 + 15) / 16 * 16;     // +4: over-read guard
+  static constexpr int SCRATCH0 = IN8_AL;                     // phase 0-2
+  static constexpr int SCRATCH1 = 3 * Conv2Cfg::WBUF;         // phase 3 (weight ring)
+  static constexpr int LDS = Conv2Cfg::PATCH + (SCRATCH0 > SCRATCH1 ? SCRATCH0 : SCRATCH1);
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+// 9 consecutive bytes of LDS at byte offset off (any alignment) as
+// (bytes 0-3, bytes 4-7, byte 8): three dword reads + v_alignbyte.
+QCN_DEV void lds_bytes9(const uint8_t* base, int off, uint32_t& w0, uint32_t& w1, uint32_t& b8) {
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(base + (off & ~3));
+  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
+  const uint32_t sh = (off & 3) * 8;
+  w0 = sh ? ((d0 >> sh) | (d1 << (32 - sh))) : d0;
+  w1 = sh ? ((d1 >> sh) | (d2 << (32 - sh))) : d1;
+  const uint32_t w2 = sh ? ((d2 >> sh) | (d3 << (32 - sh))) : d2;
+  b8 = w2 & 0xff;
+}
+
+__global__ __launch_bounds__(256, 2)
+void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
+                         const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
+                         const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
+  using C = Conv2Cfg;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* patch = lds;
+  uint8_t* in8 = lds + C::PATCH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int n = blockIdx.x >> 1;
+  const int y0 = (blockIdx.x & 1) * 16;
+
+  // phase 0: quantized input window (rows y0-2..y0+17, cols -2..33, [row][col][c])
+  // with unconditional batched loads, and conv2's patch halo = its input zp
+  {
+    constexpr int NITER = (Conv12::IN8 + 255) / 256;   // 9
+    float v[NITER];
+    bool ok[NITER];
+#pragma unroll
+    for (int k = 0; k < NITER; ++k) {
+      const int it = tid + k * 256;
+      const int itc = it < Conv12::IN8 ? it : 0;
+      const int c = itc / (Conv12::IN_R * Conv12::IN_C);
+      const int rr = (itc / Conv12::IN_C) % Conv12::IN_R, cc = itc % Conv12::IN_C;
+      const int iy = y0 - 2 + rr, ix = cc - 2;
+      ok[k] = iy >= 0 && iy < 32 && ix >= 0 && ix < 32;
+      v[k] = x[ok[k] ? (((long)n * 3 + c) * 32 + iy) * 32 + ix : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < NITER; ++k) {
+      const int it = tid + k * 256;
+      if (it >= Conv12::IN8) continue;
+      const int c = it / (Conv12::IN_R * Conv12::IN_C);
+      const int rr = (it / Conv12::IN_C) % Conv12::IN_R, cc = it % Conv12::IN_C;
+      int q = in_zp;
+      if (ok[k]) {
+        float t = v[k] * in_inv;
+        t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
+        q = (int)__builtin_rintf(t) + in_zp;
+        q = q < 0 ? 0 : (q > 255 ? 255 : q);
+      }
+      in8[(rr * Conv12::IN_C + cc) * 3 + c] = (uint8_t)(q ^ 0x80);
+    }
+    if (tid < 4) in8[Conv12::IN8 + tid] = 0;  // bytes the 9-byte reader may touch
+  }
+  const uint32_t padw = xor80(splat_u8(x2_zp));
+  const uint4 pad4 = make_uint4(padw, padw, padw, padw);
+  for (int it = tid; it < C::PROWS * C::PCOLS * 4; it += 256) {
+    const int sl = it >> 2, chunk = it & 3;
+    const int pr = sl / C::PCOLS, pc = sl % C::PCOLS;
+    const int iy = y0 + pr - 1;
+    if (iy < 0 || iy >= 32 || pc == 0 || pc == C::PCOLS - 1)
+      *reinterpret_cast<uint4*>(patch + C::slot(0, pr, pc) + chunk * 16) = pad4;
+  }
+  __syncthreads();
+
+  // phase 1+2: conv1 on MFMA, one 32-pixel row tile (patch row t) per step.
+  // Each lane builds its own B operand (pixel l32, k half hi) from the three
+  // 9-byte input runs (k = r*9 + s*3 + c), then the epilogue writes the
+  // requantized row straight into conv2's patch (as q - 128).
+  v4i a1[2];
+  v16i c1[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    a1[i] = *reinterpret_cast<const v4i*>(w1 + (i * 32 + l32) * 32 + hi * 16);
+    c1[i] = acc_init_corr(ep1.corr, i * 32, hi);
+  }
+  const EpiK k1a = load_epik(ep1, 0, hi), k1b = load_epik(ep1, 32, hi);
+  for (int t = wave; t < 18; t += 4) {
+    const int iy = y0 - 1 + t;
+    if (iy < 0 || iy >= 32) continue;  // wave-uniform: halo row keeps the pad value
+    uint32_t r0a, r0b, r0c, r1a, r1b, r1c, r2a, r2b, r2c;
+    lds_bytes9(in8, ((t + 0) * Conv12::IN_C + l32 + 1) * 3, r0a, r0b, r0c);
+    lds_bytes9(in8, ((t + 1) * Conv12::IN_C + l32 + 1) * 3, r1a, r1b, r1c);
+    lds_bytes9(in8, ((t + 2) * Conv12::IN_C + l32 + 1) * 3, r2a, r2b, r2c);
+    v4i b;
+    if (hi == 0) {  // k 0..15 = row0[0..9) + row1[0..7)
+      b = (v4i){(int)r0a, (int)r0b, (int)(r0c | (r1a << 8)), (int)((r1a >> 24) | (r1b << 8))};
+    } else {        // k 16..31 = row1[7..9) + row2[0..9) + 5 zero bytes
+      b = (v4i){(int)((r1b >> 24) | (r1c << 8) | (r2a << 16)), (int)((r2a >> 16) | (r2b << 16)),
+                (int)((r2b >> 16) | (r2c << 16)), 0};
+    }
+    uint8_t* prow_ptr = patch + C::slot(0, t, l32 + 1);
+    const v16i acc1a = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[0], b, c1[0], 0, 0, 0);
+    const v16i acc1b = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[1], b, c1[1], 0, 0, 0);
+    epilogue_tile_k<1, true>(&acc1a, k1a, ep1, 0, hi, prow_ptr);
+    epilogue_tile_k<1, true>(&acc1b, k1b, ep1, 32, hi, prow_ptr);
+  }
+
+  // phase 3: conv2 (main loop issues its weight ring over the input window,
+  // which every wave must have finished reading)
+  __syncthreads();
+  v16i acc[2][4];
+  conv_mainloop<C>(patch, lds + C::PATCH, w2, ep2.corr, wave, lane, acc);
+  conv_epilogue<C>(acc, ep2, lds, nimg, wave, lane, tid, y);
 }
 
 // --------------------------------------------------------------------------
@@ -569,6 +782,36 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
   const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(conv3x3_generic_kernel, dim3(grid), dim3(256), 0, st, x, nimg, h, w, cin,
                      x_zp, w_packed, tiled, cout, ep, pool, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
+                              const int8_t* w1_packed, const float* u1, const float* v1,
+                              const float* mult1, const int32_t* corr1, int z1, int relu1,
+                              const qcn_qdq_t* qdq1, int x2_zp, const int8_t* w2_packed,
+                              const float* u2, const float* v2, const float* mult2,
+                              const int32_t* corr2, int y_zp, int relu2, const qcn_qdq_t* qdq2,
+                              uint8_t* y, void* stream) {
+  if (!x || !w1_packed || !u1 || !v1 || !mult1 || !corr1 || !w2_packed || !u2 || !v2 || !mult2 ||
+      !corr2 || !y)
+    return QCN_ERR_ARG;
+  if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f) || x2_zp < 0 || x2_zp > 255 ||
+      y_zp < 0 || y_zp > 255 || z1 < 0 || z1 > 255)
+    return QCN_ERR_ARG;
+  ConvEpi ep1{u1, v1, mult1, corr1, z1, relu1 ? z1 : 0, 0, 0.f, 0, 0.f, 0};
+  if (qdq1) { ep1.qdq = 1; ep1.s1 = qdq1->s1; ep1.z1 = qdq1->z1; ep1.inv2 = qdq1->inv2; ep1.z2 = qdq1->z2; }
+  ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0};
+  if (qdq2) { ep2.qdq = 1; ep2.s1 = qdq2->s1; ep2.z1 = qdq2->z1; ep2.inv2 = qdq2->inv2; ep2.z2 = qdq2->z2; }
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (hipFuncSetAttribute((const void*)qcn::conv12_fused_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, qcn::Conv12::LDS) != hipSuccess)
+      return QCN_ERR_HIP;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(qcn::conv12_fused_kernel, dim3(nimg * 2), dim3(256), qcn::Conv12::LDS,
+                     (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
+                     w2_packed, ep2, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

@@ -51,7 +51,30 @@ __global__ __launch_bounds__(256) void linear_u8s8_kernel(
     wr[i] = w + (long)(f_ok[i] ? f : 0) * k + hi * 16;
   }
   v16i acc[2] = {(v16i){0}, (v16i){0}};
-  for (int kk = kb; kk < kb + kq; kk += 32) {
+  // 4 K-steps of loads in flight per batch (the loop is latency-bound otherwise)
+  constexpr int U = 4;
+  int kk = kb;
+  for (; kk + 32 * U <= kb + kq; kk += 32 * U) {
+    uint4 xb[U];
+    v4i wa[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xb[u] = *reinterpret_cast<const uint4*>(xr + kk + 32 * u);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) wa[u][i] = *reinterpret_cast<const v4i*>(wr[i] + kk + 32 * u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const v4i b = (v4i){(int)xor80(xb[u].x), (int)xor80(xb[u].y), (int)xor80(xb[u].z),
+                          (int)xor80(xb[u].w)};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const v4i a = f_ok[i] ? wa[u][i] : (v4i){0, 0, 0, 0};
+        acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[i], 0, 0, 0);
+      }
+    }
+  }
+  for (; kk < kb + kq; kk += 32) {
     uint4 xb = *reinterpret_cast<const uint4*>(xr + kk);
     const v4i b = (v4i){(int)xor80(xb.x), (int)xor80(xb.y), (int)xor80(xb.z), (int)xor80(xb.w)};
 #pragma unroll

@@ -50,6 +50,9 @@ SIGNATURES = {
                                     i32, C.POINTER(QDQ), vp, vp]),
     "qcn_conv1_f32_nchw": (i32, [vp, i32, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,
                                  C.POINTER(QDQ), vp, vp, vp]),
+    "qcn_conv12_fused_f32_nchw": (i32, [vp, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,
+                                        C.POINTER(QDQ), i32, vp, vp, vp, vp, vp, i32, i32,
+                                        C.POINTER(QDQ), vp, vp]),
     "qcn_linear_u8s8": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, f32, vp]),
     "qcn_linear_dynamic_workspace_size": (i64, [i32, i32]),
     "qcn_linear_dynamic_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp]),

@@ -150,6 +150,25 @@ def conv1_f32(x, in_scale, in_zp, w1_packed, u, v, mult, corr, y_zp, relu, qdq=N
     return out
 
 
+def conv12_fused(x, in_scale, in_zp, l1, l2, out=None):
+    """conv1 (+quantize) and conv2 (+pool) of SimpleConvNet in one launch.
+    ``l1``/``l2`` carry w, u, v, mult, corr, z_y, relu, qdq (and l2.z_x)."""
+    _need(x, torch.float32, "conv12.x")
+    n = x.shape[0]
+    if tuple(x.shape[1:]) != (3, 32, 32):
+        raise ValueError("conv12_fused expects [n,3,32,32]")
+    if out is None:
+        out = torch.empty((n, 16, 16, 64), dtype=torch.uint8, device=x.device)
+    q1 = C.byref(l1.qdq) if l1.qdq is not None else None
+    q2 = C.byref(l2.qdq) if l2.qdq is not None else None
+    check(lib().qcn_conv12_fused_f32_nchw(
+        _ptr(x), n, float(in_scale), int(in_zp), _ptr(l1.w), _ptr(l1.u), _ptr(l1.v), _ptr(l1.mult),
+        _ptr(l1.corr), int(l1.z_y), int(bool(l1.relu)), q1, int(l2.z_x), _ptr(l2.w), _ptr(l2.u),
+        _ptr(l2.v), _ptr(l2.mult), _ptr(l2.corr), int(l2.z_y), int(bool(l2.relu)), q2, _ptr(out),
+        _stream()), "conv12_fused")
+    return out
+
+
 def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=False, out=None,
               out_f=None):
     _need(x, torch.uint8, "linear.x")

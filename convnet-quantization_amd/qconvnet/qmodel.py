@@ -198,7 +198,7 @@ class QuantizedConvNet:
     """Duck-typed int8 model object (the surface of the reference's models.*:
     eval(), to() in place, cpu(), __call__; fp32 [N,3,32,32] in, fp32 [N,10] out)."""
 
-    def __init__(self, spec, device="cuda"):
+    def __init__(self, spec, device="cuda", fuse12=True):
         self.spec = spec
         self.mode = spec["mode"]
         self.device = torch.device(device)
@@ -207,6 +207,7 @@ class QuantizedConvNet:
         self.quantized = True
         self.is_custom_quantized = self.mode == "qdq"
         self.host_io = False
+        self.fuse12 = fuse12
         self._bufs = {}
         self._graphs = {}
         self._upload()
@@ -284,7 +285,9 @@ class QuantizedConvNet:
         """Launch the whole int8 forward on the current stream (no sync).
         Returns the fp32 logits tensor (a reused buffer); with keep=True also
         the dict of intermediate u8 activations.  ``marks``: a list that
-        receives 9 timing events (before conv1, after each of the 8 kernels)."""
+        receives 9 timing events (before conv1, after each of the 8 kernels;
+        with the fused conv1+conv2 launch the conv1 slot is empty and the conv2
+        slot times the fused kernel)."""
         n = x.shape[0]
         b = self._buffers(n)
         L = self.L
@@ -297,12 +300,18 @@ class QuantizedConvNet:
 
         mark()
         d = L[0]
-        ops.conv1_f32(x, self.in_scale, self.in_zp, d.w, d.u, d.v, d.mult, d.corr, d.z_y, d.relu,
-                      d.qdq, out=b["a1"])
-        mark()
-        prev = b["a1"]
         names = ["a2", "a3", "a4", "a5", "a6"]
-        for i in range(1, 6):
+        if self.fuse12 and tuple(x.shape[1:]) == (3, 32, 32):
+            ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
+            mark()
+            mark()
+            prev, first = b["a2"], 2
+        else:
+            ops.conv1_f32(x, self.in_scale, self.in_zp, d.w, d.u, d.v, d.mult, d.corr, d.z_y,
+                          d.relu, d.qdq, out=b["a1"])
+            mark()
+            prev, first = b["a1"], 1
+        for i in range(first, 6):
             d = L[i]
             ops.conv3x3(prev, d.z_x, d.w, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, d.pool,
                         d.qdq, out=b[names[i - 1]])

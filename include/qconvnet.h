@@ -101,6 +101,20 @@ int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_
                        const int32_t* corr, int y_zp, int relu, const qcn_qdq_t* qdq, uint8_t* y,
                        uint8_t* q_in, void* stream);
 
+/* A1+A5+A6+A10 fused — QuantStub + conv1(+ReLU) + conv2(+ReLU) + 2x2 max-pool
+ * of SimpleConvNet's first block (baseline_model.py:13-18, :60-63): fp32 NCHW
+ * [nimg,3,32,32] in, u8 NHWC [nimg,16,16,64] out; conv1's activation stays in
+ * LDS.  Parameters as qcn_conv1_f32_nchw (conv1: z1 = its output zero point,
+ * qdq1 its optional hand-off) and qcn_conv3x3_u8s8_nhwc (conv2: x2_zp = its
+ * input zero point). */
+int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
+                              const int8_t* w1_packed, const float* u1, const float* v1,
+                              const float* mult1, const int32_t* corr1, int z1, int relu1,
+                              const qcn_qdq_t* qdq1, int x2_zp, const int8_t* w2_packed,
+                              const float* u2, const float* v2, const float* mult2,
+                              const int32_t* corr2, int y_zp, int relu2, const qcn_qdq_t* qdq2,
+                              uint8_t* y, void* stream);
+
 /* A9 — quantized Linear / LinearReLU (fbgemm), static qparams:
  * fc1/fc2 of SimpleConvNet (baseline_model.py:38,40).
  *   x: u8 [m,k] (zero point x_zp); w: s8 [n,k] row-major; y: u8 [m,n].

@@ -215,15 +215,18 @@ def test_full_net_static_int8_golden(dev, per_channel):
     spec, _ = netfix.static_spec(z)
     assert netfix.check_weights(spec, z) == []
     x = netfix.images(z)
-    model = QuantizedConvNet(spec, dev)
-    logits, bufs = model.run(torch.from_numpy(x).to(dev), keep=True)
-    torch.cuda.synchronize()
-    assert np.array_equal(bufs["q"].cpu().numpy(), z["q_logits"])
-    assert np.array_equal(logits.cpu().numpy(), z["logits"])
-    for i, name in enumerate(["a1", "a2", "a3", "a4", "a5", "a6"], start=1):
-        assert netfix.sha(bufs[name].cpu().numpy()) == str(z[f"conv{i}_sha"]), name
-    assert netfix.sha(bufs["f1"].cpu().numpy()) == str(z["fc1_sha"])
-    assert np.array_equal(model(torch.from_numpy(x)).argmax(1).numpy(), z["argmax"])
+    for fuse in (False, True):   # unfused exposes conv1's activation; fused is the product
+        model = QuantizedConvNet(spec, dev, fuse12=fuse)
+        logits, bufs = model.run(torch.from_numpy(x).to(dev), keep=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(bufs["q"].cpu().numpy(), z["q_logits"]), fuse
+        assert np.array_equal(logits.cpu().numpy(), z["logits"]), fuse
+        for i, name in enumerate(["a1", "a2", "a3", "a4", "a5", "a6"], start=1):
+            if fuse and name == "a1":
+                continue
+            assert netfix.sha(bufs[name].cpu().numpy()) == str(z[f"conv{i}_sha"]), (name, fuse)
+        assert netfix.sha(bufs["f1"].cpu().numpy()) == str(z["fc1_sha"])
+        assert np.array_equal(model(torch.from_numpy(x)).argmax(1).numpy(), z["argmax"])
 
 
 @pytest.mark.parametrize("per_channel", [False, True])
@@ -265,3 +268,19 @@ def test_batch_split_invariance_and_graph(dev):
     out = model.replay(1024)
     torch.cuda.synchronize()
     assert torch.equal(out, torch.flip(full, [0]))
+
+
+@pytest.mark.parametrize("mode", ["static", "qdq"])
+def test_fused_conv12_equals_unfused(dev, mode):
+    """The fused conv1+conv2 launch produces the unfused pair's u8 output
+    exactly (odd batch: last workgroup pair partially outside the batch)."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    from oracle import torch_ref
+    z = netfix.load(False)
+    spec = netfix.static_spec(z)[0] if mode == "static" else netfix.qdq_spec(z)
+    x = torch.from_numpy(torch_ref.synthetic_images(37, 9) * 1.5).to(dev)
+    a = QuantizedConvNet(spec, dev, fuse12=False).run(x, keep=True)[1]["a2"].clone()
+    b = QuantizedConvNet(spec, dev, fuse12=True).run(x, keep=True)[1]["a2"].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
