@@ -41,6 +41,7 @@ PEAK_HBM_GBS = 8000.0
 MAC_PER_IMAGE = {"conv1": 1_769_472, "conv2": 37_748_736, "conv3": 18_874_368,
                  "conv4": 37_748_736, "conv5": 18_874_368, "conv6": 37_748_736,
                  "fc1": 2_097_152, "fc2": 5_120}
+MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -48,7 +49,8 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv4": 16 * 16 * 128 + 8 * 8 * 128,
                    "conv5": 8 * 8 * 128 + 8 * 8 * 256,
                    "conv6": 8 * 8 * 256 + 4 * 4 * 256,
-                   "fc1": 4096 + 512, "fc2": 512 + 10 + 40}
+                   "fc1": 4096 + 512, "fc2": 512 + 10 + 40,
+                 "conv12": 3 * 32 * 32 * 4 + 16 * 16 * 64}
 HBM_BOUND = {"conv1"}
 
 
@@ -190,7 +192,7 @@ def main():
         step(m)
         marks_all.append(m)
     torch.cuda.synchronize()
-    names = model.KERNELS
+    names = model.kernel_names(x.shape)
     per = {n: [] for n in names}
     for m in marks_all:
         for i, n in enumerate(names):

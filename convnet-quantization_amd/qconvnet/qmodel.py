@@ -280,14 +280,22 @@ class QuantizedConvNet:
 
     # --------------------------------------------------------------- forward
     KERNELS = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2")
+    KERNELS_FUSED = ("conv12", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2")
+
+    def kernel_names(self, x_shape):
+        """Names of the launches run() marks, in order (conv1+conv2 are one
+        launch when fused)."""
+        return self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS
+
+    def _fused(self, x_shape):
+        return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
 
     def run(self, x, keep=False, marks=None):
         """Launch the whole int8 forward on the current stream (no sync).
         Returns the fp32 logits tensor (a reused buffer); with keep=True also
         the dict of intermediate u8 activations.  ``marks``: a list that
-        receives 9 timing events (before conv1, after each of the 8 kernels;
-        with the fused conv1+conv2 launch the conv1 slot is empty and the conv2
-        slot times the fused kernel)."""
+        receives one timing event before the first launch and one after each
+        launch named by kernel_names(x.shape)."""
         n = x.shape[0]
         b = self._buffers(n)
         L = self.L
@@ -301,9 +309,8 @@ class QuantizedConvNet:
         mark()
         d = L[0]
         names = ["a2", "a3", "a4", "a5", "a6"]
-        if self.fuse12 and tuple(x.shape[1:]) == (3, 32, 32):
+        if self._fused(x.shape):
             ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
-            mark()
             mark()
             prev, first = b["a2"], 2
         else:

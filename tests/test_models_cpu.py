@@ -1,0 +1,57 @@
+"""CPU checks of the drop-in model surface (no GPU): checkpoint ingestion
+(main.py:22-26 / model_trainer.py:93-99 format), SimpleConvNet state-dict keys
+and fp32 forward against the oracle's restatement of baseline_model.py:13-83,
+and the loud failure of the int8 path on a non-GPU device."""
+import pytest
+import torch
+
+from models.baseline_model import SimpleConvNet, load_checkpoint_state, synthetic_model
+from oracle import torch_ref
+
+
+def test_checkpoint_formats_load(tmp_path):
+    m = SimpleConvNet()
+    sd = m.state_dict()
+    ckpt = {"epoch": 3, "model_state_dict": sd, "optimizer_state_dict": {}, "best_accuracy": 0.5}
+    torch.save(ckpt, tmp_path / "best.pth")
+    torch.save(sd, tmp_path / "bare.pth")
+    for f in ("best.pth", "bare.pth"):
+        obj = torch.load(tmp_path / f, weights_only=True)
+        m2 = SimpleConvNet()
+        m2.load_state_dict(load_checkpoint_state(obj))
+        for k, v in sd.items():
+            assert torch.equal(m2.state_dict()[k], v), k
+
+
+def test_state_dict_keys_match_reference_topology():
+    ours = SimpleConvNet().state_dict()
+    ref = torch_ref.SimpleConvNetRef().state_dict()
+    assert list(ours.keys()) == list(ref.keys())
+    for k in ours:
+        assert ours[k].shape == ref[k].shape, k
+
+
+def test_fp32_forward_matches_restatement():
+    from qconvnet import data
+    calib = torch.from_numpy(data.synthetic_images(64, 1))
+    m = synthetic_model(0, calib)
+    r = torch_ref.SimpleConvNetRef()
+    r.load_state_dict(m.state_dict())
+    r.eval()
+    x = torch.from_numpy(data.synthetic_images(16, 5))
+    with torch.no_grad():
+        assert torch.allclose(m(x), r(x), rtol=1e-5, atol=1e-5)
+
+
+def test_static_ptq_wrapper_rejects_cpu_device():
+    from models.static_ptq_model import StaticPTQModel
+    from qconvnet.qmodel import QuantizedConvNet
+    with pytest.raises(ValueError):
+        QuantizedConvNet({"mode": "static"}, "cpu")
+    from qconvnet import data
+    sp = StaticPTQModel(device="cpu")
+    sp.load_state_dict(SimpleConvNet().state_dict())
+    assert hasattr(sp, "fp32_model")
+    # calibration runs on the host, but the int8 model itself refuses the CPU
+    with pytest.raises(ValueError):
+        sp.quantize(torch.from_numpy(data.synthetic_images(8, 1)))
