@@ -14,6 +14,7 @@
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 #define QCN_DEV __device__ __forceinline__
 
@@ -71,3 +72,19 @@ QCN_DEV uint32_t splat_u8(int b) {
   uint32_t x = (uint32_t)(b & 0xff);
   return x | (x << 8) | (x << 16) | (x << 24);
 }
+
+// 16-B-per-lane LDS-DMA (global_load_lds_dwordx4) issued from inline asm.
+// The compiler's wait-count model treats an in-flight builtin LDS-DMA as an
+// LDS event of unknown order and then guards every later ds_read use with
+// lgkmcnt(0), which serialises a software-pipelined MFMA loop.  Callers of
+// this form track completion themselves with explicit s_waitcnt vmcnt.
+// lds_dst: the wave's 1-KiB destination (lane i writes lds_dst + 16 i).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0 is ours for the two instructions
+QCN_DEV void glds16(const void* gsrc, void* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(gsrc), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop

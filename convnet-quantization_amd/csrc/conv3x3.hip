@@ -25,6 +25,21 @@
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
 
+// Diagnostic build only (tools/micro/conv_stamp.hip defines QCN_STAMPS):
+// wave 0 of each workgroup records s_memtime at phase boundaries.
+#ifdef QCN_STAMPS
+__device__ unsigned long long qcn_stamps[1 << 16][8];
+#define QCN_STAMP(k)                                                              \
+  do {                                                                            \
+    if (threadIdx.x == 0) {                                                       \
+      qcn_stamps[blockIdx.x & 0xffff][k] = __builtin_amdgcn_s_memtime();          \
+      if (k == 0 || k == 5) qcn_stamps[blockIdx.x & 0xffff][6 + k / 5] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                             \
+  } while (0)
+#else
+#define QCN_STAMP(k) do {} while (0)
+#endif
+
 namespace qcn {
 
 // Patch layout knobs (chosen per layer by an offline bank-conflict search so
@@ -58,7 +73,8 @@ struct ConvCfg {
   static constexpr int OS = COUT + 16;           // output staging row stride
   static constexpr int MAIN = PATCH + 3 * WBUF;  // patch + 3-deep weight ring
   static constexpr int OUT = OPX * OS;
-  static constexpr int LDS = MAIN > OUT ? MAIN : OUT;
+  static constexpr int EPI = MAIN > OUT ? MAIN : OUT;  // u | v | mult (fp32 x COUT each)
+  static constexpr int LDS = EPI + 12 * COUT;
   static_assert(CIN % 64 == 0 && COUT % 64 == 0, "channel multiples of 64");
   static_assert(PSP % 16 == 0 && RPAD % 16 == 0 && SPAD % 16 == 0, "16-B aligned layout");
   static_assert(PXB % W == 0, "workgroup covers whole rows");
@@ -107,7 +123,40 @@ QCN_DEV EpiK load_epik(const ConvEpi& ep, int co_base, int hi) {
   return k;
 }
 
-template <int NQ, bool XORIN = false>
+// Same constants from the workgroup's LDS copy (stage_epik): broadcast reads
+// instead of per-tile global loads in the epilogue.
+QCN_DEV EpiK load_epik_lds(const float* ek, int cout, int co_base, int hi) {
+  EpiK k;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int co = co_base + 8 * g + 4 * hi;
+    const float4 u4 = *reinterpret_cast<const float4*>(ek + co);
+    const float4 v4 = *reinterpret_cast<const float4*>(ek + cout + co);
+    const float4 m4 = *reinterpret_cast<const float4*>(ek + 2 * cout + co);
+    k.u[4 * g] = u4.x; k.u[4 * g + 1] = u4.y; k.u[4 * g + 2] = u4.z; k.u[4 * g + 3] = u4.w;
+    k.v[4 * g] = v4.x; k.v[4 * g + 1] = v4.y; k.v[4 * g + 2] = v4.z; k.v[4 * g + 3] = v4.w;
+    k.m[4 * g] = m4.x; k.m[4 * g + 1] = m4.y; k.m[4 * g + 2] = m4.z; k.m[4 * g + 3] = m4.w;
+  }
+  return k;
+}
+
+// Copy u | v | mult (COUT floats each) into LDS at ek; called in the prologue
+// so the loads overlap the patch staging (visible after the main loop's barriers).
+template <int COUT, int NT>
+QCN_DEV void stage_epik(const ConvEpi& ep, float* ek, int tid) {
+  for (int e = tid; e < 3 * COUT / 4; e += NT) {
+    const int arr = e / (COUT / 4), o = (e % (COUT / 4)) * 4;
+    const float* src = arr == 0 ? ep.u : (arr == 1 ? ep.v : ep.mult);
+    *reinterpret_cast<float4*>(ek + arr * COUT + o) = *reinterpret_cast<const float4*>(src + o);
+  }
+}
+
+// FAST: zp_y == 0, lo == 0 and no QDQ hand-off (every post-ReLU layer of the
+// static net).  Then clamp(rne(ab) + zp, lo, 255) == v_cvt_pk_u8_f32(ab), which
+// rounds half-to-even and saturates to [0, 255] (probed exhaustively on gfx950,
+// tools/micro/cvt_probe.hip), and the fma / mul run as packed fp32 pairs:
+// 3 VALU per element instead of 7 (the epilogue is VALU-issue bound).
+template <int NQ, bool XORIN, bool FAST>
 QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
                              int hi, uint8_t* orow) {
   // accumulators already include the zero-point correction (acc_init_corr)
@@ -117,14 +166,32 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     uint32_t wd = 0;
+    int a[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int rg = 4 * g + e;
-      int a = accs[0][rg];
-      if constexpr (NQ == 4) a = max(max(a, accs[1][rg]), max(accs[2][rg], accs[3][rg]));
-      float q = requant_f(a, K.u[rg], K.v[rg], K.m[rg], zpf, lof);
-      if (ep.qdq) q = qdq_next_f(q, ep.s1, z1f, ep.inv2, z2f);
-      wd = __builtin_amdgcn_cvt_pk_u8_f32(q, e, wd);
+      a[e] = accs[0][rg];
+      if constexpr (NQ == 4) a[e] = max(max(a[e], accs[1][rg]), max(accs[2][rg], accs[3][rg]));
+    }
+    if constexpr (FAST) {
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int rg = 4 * g + e;
+        const v2f af = {(float)a[e], (float)a[e + 1]};
+        const v2f t = __builtin_elementwise_fma((v2f){K.u[rg], K.u[rg + 1]},
+                                                (v2f){K.v[rg], K.v[rg + 1]}, af);
+        const v2f ab = t * (v2f){K.m[rg], K.m[rg + 1]};
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.x, e, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rg = 4 * g + e;
+        float q = requant_f(a[e], K.u[rg], K.v[rg], K.m[rg], zpf, lof);
+        if (ep.qdq) q = qdq_next_f(q, ep.s1, z1f, ep.inv2, z2f);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(q, e, wd);
+      }
     }
     w[g] = wd;
   }
@@ -143,10 +210,19 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
   *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+QCN_DEV bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
+
+template <int NQ, bool XORIN = false>
+QCN_DEV void epilogue_tile_kf(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
+                              int hi, uint8_t* orow) {
+  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true>(accs, K, ep, co_base, hi, orow);
+  else epilogue_tile_k<NQ, XORIN, false>(accs, K, ep, co_base, hi, orow);
+}
+
 template <int NQ, bool XORIN = false>
 QCN_DEV void epilogue_tile(const v16i* accs, const ConvEpi& ep, int co_base, int hi,
                            uint8_t* orow) {
-  epilogue_tile_k<NQ, XORIN>(accs, load_epik(ep, co_base, hi), ep, co_base, hi, orow);
+  epilogue_tile_kf<NQ, XORIN>(accs, load_epik(ep, co_base, hi), ep, co_base, hi, orow);
 }
 
 // Accumulator tile initialised with the zero-point correction
@@ -197,6 +273,13 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // (swizzle applied on the SOURCE address, the LDS image stays lane-linear)
   // so the A-operand ds_read_b128 of 16 consecutive rows is conflict-free.
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_g = [&](int ch, int g) {
+    uint8_t* buf = wring + (ch % 3) * C::WBUF;
+    const int8_t* base = wpk + (long)ch * C::WBUF;
+    const int o = (g * C::NWAVES + wave_u) * 1024 + lane * 16;
+    const int r = o >> 6, sl = (o >> 4) & 3;
+    glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
+  };
   auto issue = [&](int ch) {
     uint8_t* buf = wring + (ch % 3) * C::WBUF;
     const int8_t* base = wpk + (long)ch * C::WBUF;
@@ -204,9 +287,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
     for (int g = 0; g < C::NG; ++g) {
       const int o = (g * C::NWAVES + wave_u) * 1024 + lane * 16;
       const int r = o >> 6, sl = (o >> 4) & 3;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4)),
-          (void*)(buf + (g * C::NWAVES + wave_u) * 1024), 16, 0, 0);
+      glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
     }
   };
 
@@ -243,45 +324,92 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   if (C::NCH > 1) issue(1);
   if (C::NCH > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
 
+  // Software pipeline over (chunk, kk) steps: the fragments of step s+1 are
+  // read from LDS while the 8 MFMAs of step s run.  Chunk ch+1's weights are
+  // needed from step (ch, 1) on, so that step waits for its DMA and passes the
+  // workgroup barrier first; the same barrier proves every wave has consumed
+  // chunk ch-1 (read during step (ch-1,0), used by step (ch-1,1)), so the DMA
+  // of ch+2 into that buffer is issued right after it.
+  constexpr int CB = CIN / 64;
+  v4i fa0[2], fb0[4], fa1[2], fb1[4];
+  auto tap_addr = [&](int tap, int (&pa)[4]) {
+    const int r = tap / 3, s = tap % 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pa[j] = C::slot(pseg[j], prow[j] + r, pcol[j] + s) + hi * 16;
+  };
+  auto rd = [&](v4i (&fa)[2], v4i (&fb)[4], int ch, int cb, int kk, const int (&pa)[4]) {
+    const uint8_t* wb = wring + (ch % 3) * C::WBUF + arow * 64;
+    const int aoff = ((2 * kk + hi) ^ aswz) << 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(wb + i * 32 * 64 + aoff);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      fb[j] = *reinterpret_cast<const v4i*>(patch + pa[j] + cb * 64 + kk * 32);
+  };
+  auto mm = [&](const v4i (&fa)[2], const v4i (&fb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+  auto mm_one = [&](int i, int j, const v4i (&fa)[2], const v4i (&fb)[4]) {
+    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  };
+  // keep each step's next-step reads ahead of its MFMAs (the compiler
+  // otherwise sinks them behind the MFMAs and exposes their latency)
+  auto pin = [&]() { __builtin_amdgcn_sched_barrier(0); };
+
+  int pa[4], pn[4];
+  tap_addr(0, pa);
+  rd(fa0, fb0, 0, 0, 0, pa);
 #pragma unroll 1
   for (int tap = 0; tap < 9; ++tap) {
-    const int r = tap / 3, s = tap % 3;
-    int paddr[4];
+    tap_addr(tap < 8 ? tap + 1 : tap, pn);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) paddr[j] = C::slot(pseg[j], prow[j] + r, pcol[j] + s) + hi * 16;
-#pragma unroll
-    for (int cb = 0; cb < CIN / 64; ++cb) {
-      const int ch = tap * (CIN / 64) + cb;
-      const bool more = ch + 2 < C::NCH;
-      if (more) issue(ch + 2);
-      const uint8_t* wb = wring + (ch % 3) * C::WBUF + arow * 64;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        v4i a[2], b[4];
-        const int aoff = ((2 * kk + hi) ^ aswz) << 4;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          a[i] = *reinterpret_cast<const v4i*>(wb + i * 32 * 64 + aoff);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          b[j] = *reinterpret_cast<const v4i*>(patch + paddr[j] + cb * 64 + kk * 32);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-      // chunk ch+1 must have landed before the barrier that precedes its reads
-      if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int cb = 0; cb < CB; ++cb) {
+      const int ch = tap * CB + cb;
+      // step (ch, 0): read (ch, 1), multiply (ch, 0)
+      rd(fa1, fb1, ch, cb, 1, pa);
+      pin();
+      mm(fa0, fb0);
+      // step (ch, 1): chunk ch+1 landed and visible -> read (ch+1, 0), multiply
+      // (ch, 1).  The body stays branch-free around the MFMAs: after the last
+      // chunk the "next" reads hit a stale buffer (in bounds) and are unused.
+      __builtin_amdgcn_sched_barrier(0);   // chunk ch-1's reads stay before the barrier
+#ifndef QCN_EXP_NOBAR
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      if (cb + 1 < CB) rd(fa0, fb0, ch + 1, cb + 1, 0, pa);
+      else rd(fa0, fb0, ch + 1, 0, 0, pn);
+      pin();
+      // the LDS-DMA of chunk ch+2 is issued between MFMAs (an MFMA leaves the
+      // wave's issue port free for most of its cycles); issued up front it
+      // stalled the SIMD for its full issue cost every chunk
+      const bool dma = ch + 2 < C::NCH;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        mm_one(m >> 2, m & 3, fa1, fb1);
+#pragma unroll
+        for (int g = 0; g < C::NG; ++g)
+          if (m == (2 * g + 1) * 8 / (2 * C::NG)) {  // spread the pieces over the MFMAs
+            pin();
+            if (dma) issue_g(ch + 2, g);
+            pin();
+          }
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pa[j] = pn[j];
   }
-
+  // every wave's last reads are consumed; the caller reuses the LDS
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
 }
 
 // Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
@@ -294,21 +422,25 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
   constexpr bool POOL = C::kPool;
   constexpr int COUT = C::kCout;
   uint8_t* lout = lds;  // the patch / weight ring is dead after the last barrier
+  const float* ek = reinterpret_cast<const float*>(lds + C::EPI);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int co_base = wc * 64 + i * 32;
+    const EpiK K = load_epik_lds(ek, COUT, co_base, hi);
     if constexpr (POOL) {
       const int opx = wp * 32 + l32;
-      epilogue_tile<4>(acc[i], ep, co_base, hi, lout + opx * C::OS);
+      epilogue_tile_kf<4>(acc[i], K, ep, co_base, hi, lout + opx * C::OS);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int opx = (wp * 4 + j) * 32 + l32;
-        epilogue_tile<1>(&acc[i][j], ep, co_base, hi, lout + opx * C::OS);
+        epilogue_tile_kf<1>(&acc[i][j], K, ep, co_base, hi, lout + opx * C::OS);
       }
     }
   }
+  QCN_STAMP(3);
   __syncthreads();
+  QCN_STAMP(4);
   const long out0 = (long)blockIdx.x * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
   store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
@@ -327,6 +459,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int lane = tid & 63;
   const int wave = tid >> 6;
 
+  QCN_STAMP(0);
   const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
   const int n0 = (int)(p0 / C::IMG);
   const int y0 = (int)((p0 % C::IMG) / C::W);
@@ -335,6 +468,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   // Loads are issued in unconditional batches (halo / tail lanes read a valid
   // dummy address and are replaced afterwards) so a thread keeps BATCH 16-B
   // loads in flight instead of one dependent HBM round trip per element.
+  stage_epik<COUT, C::NT>(ep, reinterpret_cast<float*>(lds + C::EPI), tid);
   const uint32_t padw = xor80(splat_u8(x_zp));
   constexpr int CH16 = CIN / 16;
   constexpr int NSLOT = C::SEGS * C::PROWS * C::PCOLS;
@@ -367,9 +501,12 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
     }
   }
 
+  QCN_STAMP(1);
   v16i acc[2][4];
   conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
+  QCN_STAMP(2);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
+  QCN_STAMP(5);
 }
 
 // --------------------------------------------------------------------------
@@ -497,7 +634,10 @@ struct Conv12 {
   static constexpr int IN8_AL = (IN8 + 4 + 15) / 16 * 16;     // +4: over-read guard
   static constexpr int SCRATCH0 = IN8_AL;                     // phase 0-2
   static constexpr int SCRATCH1 = 3 * Conv2Cfg::WBUF;         // phase 3 (weight ring)
-  static constexpr int LDS = Conv2Cfg::PATCH + (SCRATCH0 > SCRATCH1 ? SCRATCH0 : SCRATCH1);
+  static constexpr int MAIN = Conv2Cfg::PATCH + (SCRATCH0 > SCRATCH1 ? SCRATCH0 : SCRATCH1);
+  // conv_epilogue reads conv2's constants at Conv2Cfg::EPI
+  static_assert(Conv2Cfg::EPI >= MAIN, "epilogue constants outside the scratch");
+  static constexpr int LDS = Conv2Cfg::LDS;
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
 };
 
@@ -559,6 +699,7 @@ void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, in
     }
     if (tid < 4) in8[Conv12::IN8 + tid] = 0;  // bytes the 9-byte reader may touch
   }
+  stage_epik<64, 256>(ep2, reinterpret_cast<float*>(lds + C::EPI), tid);
   const uint32_t padw = xor80(splat_u8(x2_zp));
   const uint4 pad4 = make_uint4(padw, padw, padw, padw);
   for (int it = tid; it < C::PROWS * C::PCOLS * 4; it += 256) {
@@ -599,8 +740,8 @@ void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, in
     uint8_t* prow_ptr = patch + C::slot(0, t, l32 + 1);
     const v16i acc1a = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[0], b, c1[0], 0, 0, 0);
     const v16i acc1b = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[1], b, c1[1], 0, 0, 0);
-    epilogue_tile_k<1, true>(&acc1a, k1a, ep1, 0, hi, prow_ptr);
-    epilogue_tile_k<1, true>(&acc1b, k1b, ep1, 32, hi, prow_ptr);
+    epilogue_tile_kf<1, true>(&acc1a, k1a, ep1, 0, hi, prow_ptr);
+    epilogue_tile_kf<1, true>(&acc1b, k1b, ep1, 32, hi, prow_ptr);
   }
 
   // phase 3: conv2 (main loop issues its weight ring over the input window,
