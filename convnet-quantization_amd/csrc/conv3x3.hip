@@ -24,6 +24,7 @@
 //  * for pooled layers a wave's four pixel tiles are the four 2x2-window
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
+#include <type_traits>
 
 // Diagnostic build only (tools/micro/conv_stamp.hip defines QCN_STAMPS):
 // wave 0 of each workgroup records s_memtime at phase boundaries.
@@ -51,7 +52,7 @@ template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD 
           int SPAD = 0, bool SPLIT = false>
 struct ConvCfg {
   static constexpr int kCin = CIN, kCout = COUT;
-  static constexpr bool kPool = POOL;
+  static constexpr bool kPool = POOL, kSplit = SPLIT;
   static constexpr int W = HW, H = HW;
   static constexpr int WCO = COUT / 64;          // waves along cout
   static constexpr int NWAVES = WCO * WPX;
@@ -255,16 +256,59 @@ QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long va
   }
 }
 
+// Per-lane B-operand (pixel) addressing shared by both main loops: the patch
+// address of tap (r, s) is the tap-(0,0) address plus a per-(tap, j) constant —
+// with the parity-split column order (pooled layers only) the column step
+// depends on the pixel column's parity, which is (j & 1) for pooled tiles — so
+// a fully unrolled K loop reads with immediate offsets and no address math.
+template <class C>
+struct PatchAddr {
+  static_assert(!C::kSplit || C::kPool, "parity-split columns need pooled tiles");
+  int base[4];
+  QCN_DEV PatchAddr(int wp, int l32, int hi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int seg, prow, pcol;
+      if constexpr (C::kPool) {
+        constexpr int PW = C::W / 2, PR = C::R / 2;
+        const int q = wp * 32 + l32;
+        seg = q / (PR * PW);
+        prow = 2 * ((q / PW) % PR) + (j >> 1);
+        pcol = 2 * (q % PW) + (j & 1);
+      } else {
+        const int m = (wp * 4 + j) * 32 + l32;
+        seg = m / (C::R * C::W);
+        prow = (m / C::W) % C::R;
+        pcol = m % C::W;
+      }
+      base[j] = C::slot(seg, prow, pcol) + hi * 16;
+    }
+  }
+  static constexpr int delta(int tap, int j) {
+    const int r = tap / 3, s = tap % 3;
+    int dc = s;
+    if (C::kSplit) dc = s == 0 ? 0 : (s == 2 ? 1 : ((j & 1) ? 1 - C::HALF : C::HALF));
+    return r * C::RS + dc * C::PS;
+  }
+};
+
 // Main MFMA loop over the 9 taps x CIN/64 K-chunks for a patch already staged
 // in LDS (q - 128 bytes, layout C::slot).  Weights stream through a 3-deep
 // LDS-DMA ring at wring.  Entered with all waves' patch writes issued (the
 // caller's loads may still be in flight); returns with the ring drained and all
 // waves past a barrier.
+//
+// Software pipeline over (chunk, kk) steps, fully unrolled: the fragments of
+// step s+1 are read from LDS one per MFMA of step s (a burst of 6 reads ahead
+// of the MFMAs measured 30 % slower, interleaved 8 %: tools/micro/mfma_lds.hip).
+// Chunk ch+1's weights are needed from step (ch, 1) on, so that step waits for
+// its DMA and passes the workgroup barrier first; the same barrier proves every
+// wave has consumed chunk ch-1 (read during step (ch-1,0), used by step
+// (ch-1,1)), so the DMA of ch+2 into that buffer is issued during that step.
 template <class C>
 QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* __restrict__ wpk,
                            const int* __restrict__ corr, int wave, int lane, v16i (&acc)[2][4]) {
-  constexpr int CIN = C::kCin;
-  constexpr bool POOL = C::kPool;
+  constexpr int CB = C::kCin / 64;
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
   // weight ring: K-chunk ch (64 input channels of one tap, all COUT rows
@@ -280,132 +324,80 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
     const int r = o >> 6, sl = (o >> 4) & 3;
     glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
   };
-  auto issue = [&](int ch) {
-    uint8_t* buf = wring + (ch % 3) * C::WBUF;
-    const int8_t* base = wpk + (long)ch * C::WBUF;
-#pragma unroll
-    for (int g = 0; g < C::NG; ++g) {
-      const int o = (g * C::NWAVES + wave_u) * 1024 + lane * 16;
-      const int r = o >> 6, sl = (o >> 4) & 3;
-      glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
-    }
-  };
-
-  // ---- per-lane patch positions of the four pixel tiles (tap (0,0), channel 0)
-  int pseg[4], prow[4], pcol[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if constexpr (POOL) {
-      constexpr int PW = C::W / 2, PR = C::R / 2;
-      const int q = wp * 32 + l32;
-      pseg[j] = q / (PR * PW);
-      prow[j] = 2 * ((q / PW) % PR) + (j >> 1);
-      pcol[j] = 2 * (q % PW) + (j & 1);
-    } else {
-      const int m = (wp * 4 + j) * 32 + l32;
-      pseg[j] = m / (C::R * C::W);
-      prow[j] = (m / C::W) % C::R;
-      pcol[j] = m % C::W;
-    }
-  }
+  const PatchAddr<C> pa(wp, l32, hi);
   // A operand: row wc*64 + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
   const int arow = wc * 64 + l32;
   const int aswz = (arow >> 2) & 3;  // same for arow + 32
-
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const v16i c0 = acc_init_corr(corr, wc * 64 + i * 32, hi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = c0;
   }
-
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch + corr loads retired
-  issue(0);
-  if (C::NCH > 1) issue(1);
-  if (C::NCH > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < C::NG; ++g) issue_g(0, g);
+  if constexpr (C::NCH > 1) {
+#pragma unroll
+    for (int g = 0; g < C::NG; ++g) issue_g(1, g);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::NG) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  // Software pipeline over (chunk, kk) steps: the fragments of step s+1 are
-  // read from LDS while the 8 MFMAs of step s run.  Chunk ch+1's weights are
-  // needed from step (ch, 1) on, so that step waits for its DMA and passes the
-  // workgroup barrier first; the same barrier proves every wave has consumed
-  // chunk ch-1 (read during step (ch-1,0), used by step (ch-1,1)), so the DMA
-  // of ch+2 into that buffer is issued right after it.
-  constexpr int CB = CIN / 64;
+  const uint8_t* abase = wring + arow * 64;
+  auto rd_a = [&](int ch, int kk, int i) {
+    return *reinterpret_cast<const v4i*>(abase + (ch % 3) * C::WBUF + i * 32 * 64 +
+                                         (((2 * kk + hi) ^ aswz) << 4));
+  };
+  auto rd_b = [&](int ch, int kk, int j) {
+    const int tap = ch / CB, cb = ch % CB;
+    return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 +
+                                         kk * 32);
+  };
+  // one step: 8 MFMAs on (fa, fb); reads of step (rch, rkk) into (fan, fbn)
+  // interleaved; DMA pieces of chunk dch spread over the MFMAs
+  auto step = [&](v4i (&fan)[2], v4i (&fbn)[4], int rch, int rkk, bool rd,
+                  const v4i (&fa)[2], const v4i (&fb)[4], bool dma, int dch) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (rd) {
+        if (m < 2) fan[m] = rd_a(rch, rkk, m);
+        else if (m < 6) fbn[m - 2] = rd_b(rch, rkk, m - 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc[m >> 2][m & 3] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m >> 2], fb[m & 3], acc[m >> 2][m & 3], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < C::NG; ++g)
+        if (dma && m == (2 * g + 1) * 8 / (2 * C::NG)) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue_g(dch, g);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   v4i fa0[2], fb0[4], fa1[2], fb1[4];
-  auto tap_addr = [&](int tap, int (&pa)[4]) {
-    const int r = tap / 3, s = tap % 3;
+  fa0[0] = rd_a(0, 0, 0);
+  fa0[1] = rd_a(0, 0, 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pa[j] = C::slot(pseg[j], prow[j] + r, pcol[j] + s) + hi * 16;
-  };
-  auto rd = [&](v4i (&fa)[2], v4i (&fb)[4], int ch, int cb, int kk, const int (&pa)[4]) {
-    const uint8_t* wb = wring + (ch % 3) * C::WBUF + arow * 64;
-    const int aoff = ((2 * kk + hi) ^ aswz) << 4;
+  for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const v4i*>(wb + i * 32 * 64 + aoff);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j] = *reinterpret_cast<const v4i*>(patch + pa[j] + cb * 64 + kk * 32);
-  };
-  auto mm = [&](const v4i (&fa)[2], const v4i (&fb)[4]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-  auto mm_one = [&](int i, int j, const v4i (&fa)[2], const v4i (&fb)[4]) {
-    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-  };
-  // keep each step's next-step reads ahead of its MFMAs (the compiler
-  // otherwise sinks them behind the MFMAs and exposes their latency)
-  auto pin = [&]() { __builtin_amdgcn_sched_barrier(0); };
-
-  int pa[4], pn[4];
-  tap_addr(0, pa);
-  rd(fa0, fb0, 0, 0, 0, pa);
-#pragma unroll 1
-  for (int tap = 0; tap < 9; ++tap) {
-    tap_addr(tap < 8 ? tap + 1 : tap, pn);
-#pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      const int ch = tap * CB + cb;
-      // step (ch, 0): read (ch, 1), multiply (ch, 0)
-      rd(fa1, fb1, ch, cb, 1, pa);
-      pin();
-      mm(fa0, fb0);
-      // step (ch, 1): chunk ch+1 landed and visible -> read (ch+1, 0), multiply
-      // (ch, 1).  The body stays branch-free around the MFMAs: after the last
-      // chunk the "next" reads hit a stale buffer (in bounds) and are unused.
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    // step (ch, 0): read (ch, 1), multiply (ch, 0)
+    step(fa1, fb1, ch, 1, true, fa0, fb0, false, 0);
+    if (ch + 1 < C::NCH) {
+      // step (ch, 1): chunk ch+1 landed and visible -> read (ch+1, 0), multiply (ch, 1)
       __builtin_amdgcn_sched_barrier(0);   // chunk ch-1's reads stay before the barrier
-#ifndef QCN_EXP_NOBAR
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-#endif
       __builtin_amdgcn_sched_barrier(0);
-      if (cb + 1 < CB) rd(fa0, fb0, ch + 1, cb + 1, 0, pa);
-      else rd(fa0, fb0, ch + 1, 0, 0, pn);
-      pin();
-      // the LDS-DMA of chunk ch+2 is issued between MFMAs (an MFMA leaves the
-      // wave's issue port free for most of its cycles); issued up front it
-      // stalled the SIMD for its full issue cost every chunk
-      const bool dma = ch + 2 < C::NCH;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        mm_one(m >> 2, m & 3, fa1, fb1);
-#pragma unroll
-        for (int g = 0; g < C::NG; ++g)
-          if (m == (2 * g + 1) * 8 / (2 * C::NG)) {  // spread the pieces over the MFMAs
-            pin();
-            if (dma) issue_g(ch + 2, g);
-            pin();
-          }
-      }
+      step(fa0, fb0, ch + 1, 0, true, fa1, fb1, ch + 2 < C::NCH, ch + 2);
+    } else {
+      step(fa0, fb0, 0, 0, false, fa1, fb1, false, 0);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) pa[j] = pn[j];
   }
   // every wave's last reads are consumed; the caller reuses the LDS
   __builtin_amdgcn_sched_barrier(0);
@@ -438,7 +430,6 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
       }
     }
   }
-  QCN_STAMP(3);
   __syncthreads();
   QCN_STAMP(4);
   const long out0 = (long)blockIdx.x * C::OPX;
@@ -502,9 +493,10 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   }
 
   QCN_STAMP(1);
+  QCN_STAMP(2);
   v16i acc[2][4];
   conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
-  QCN_STAMP(2);
+  QCN_STAMP(3);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
   QCN_STAMP(5);
 }
@@ -665,6 +657,7 @@ void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, in
   const int l32 = lane & 31, hi = lane >> 5;
   const int n = blockIdx.x >> 1;
   const int y0 = (blockIdx.x & 1) * 16;
+  QCN_STAMP(0);
 
   // phase 0: quantized input window (rows y0-2..y0+17, cols -2..33, [row][col][c])
   // with unconditional batched loads, and conv2's patch halo = its input zp
@@ -711,6 +704,7 @@ void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, in
   }
   __syncthreads();
 
+  QCN_STAMP(1);
   // phase 1+2: conv1 on MFMA, one 32-pixel row tile (patch row t) per step.
   // Each lane builds its own B operand (pixel l32, k half hi) from the three
   // 9-byte input runs (k = r*9 + s*3 + c), then the epilogue writes the
@@ -747,9 +741,393 @@ void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, in
   // phase 3: conv2 (main loop issues its weight ring over the input window,
   // which every wave must have finished reading)
   __syncthreads();
+  QCN_STAMP(2);
   v16i acc[2][4];
   conv_mainloop<C>(patch, lds + C::PATCH, w2, ep2.corr, wave, lane, acc);
+  QCN_STAMP(3);
   conv_epilogue<C>(acc, ep2, lds, nimg, wave, lane, tid, y);
+  QCN_STAMP(5);
+}
+
+// --------------------------------------------------------------------------
+// conv1 + conv2 fused, persistent and wave-specialised (the production path).
+// One 512-thread workgroup per CU loops over half-image tiles.  Waves 4-7
+// (producer) build conv2's input patch for tile j — fp32 window -> quantize ->
+// conv1 on MFMA -> requant into the patch — while waves 0-3 (consumer) run
+// conv2 on tile j-1 from the other patch buffer and store its pooled output.
+// conv2's weights (36 KB) stay resident in LDS, so the consumer loop has no
+// barriers and no weight traffic; the only synchronisation is one workgroup
+// barrier per tile.  The producer's VALU-heavy conv1 and the consumer's MFMA
+// work share the SIMDs instead of alternating.  The fp32 window of tile j+1 is
+// loaded into registers at the start of the producer's phase, so its latency
+// hides behind the conv1 work.
+struct Conv12P {
+  using C = Conv2Cfg;
+  static constexpr int PATCH = C::PATCH;
+  static constexpr int WRES = 9 * C::WBUF;                 // all conv2 weights
+  static constexpr int OFF_W = 2 * PATCH;
+  static constexpr int OFF_IN = OFF_W + WRES;              // 2 x quantized input window
+  static constexpr int OFF_EPI1 = OFF_IN + 2 * Conv12::IN8_AL;
+  static constexpr int OFF_EPI2 = OFF_EPI1 + 12 * 64;
+  static constexpr int OFF_CORR2 = OFF_EPI2 + 12 * 64;      // conv2 corr (int32 x 64)
+  static constexpr int LDS = OFF_CORR2 + 4 * 64;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// conv_mainloop for weights resident in LDS (same swizzled chunk layout as the
+// ring, chunk ch at wres + ch * WBUF): a barrier-free, fully unrolled pipeline.
+template <class C>
+QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
+                               const int* __restrict__ corr, int wave, int lane,
+                               v16i (&acc)[2][4]) {
+  constexpr int CB = C::kCin / 64;
+  const int wc = wave % C::WCO, wp = wave / C::WCO;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const PatchAddr<C> pa(wp, l32, hi);
+  const int arow = wc * 64 + l32;
+  const int aswz = (arow >> 2) & 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const v16i c0 = acc_init_corr(corr, wc * 64 + i * 32, hi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
+  }
+  const uint8_t* abase = wres + arow * 64;
+  auto rd_a = [&](int ch, int kk, int i) {
+    return *reinterpret_cast<const v4i*>(abase + ch * C::WBUF + i * 32 * 64 +
+                                         (((2 * kk + hi) ^ aswz) << 4));
+  };
+  auto rd_b = [&](int ch, int kk, int j) {
+    const int tap = ch / CB, cb = ch % CB;
+    return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 +
+                                         kk * 32);
+  };
+  auto step = [&](v4i (&fan)[2], v4i (&fbn)[4], int rch, int rkk, bool rd,
+                  const v4i (&fa)[2], const v4i (&fb)[4]) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (rd) {
+        if (m < 2) fan[m] = rd_a(rch, rkk, m);
+        else if (m < 6) fbn[m - 2] = rd_b(rch, rkk, m - 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc[m >> 2][m & 3] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m >> 2], fb[m & 3], acc[m >> 2][m & 3], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  v4i fa0[2], fb0[4], fa1[2], fb1[4];
+  fa0[0] = rd_a(0, 0, 0);
+  fa0[1] = rd_a(0, 0, 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
+#pragma unroll
+  for (int ch = 0; ch < C::NCH; ++ch) {
+    step(fa1, fb1, ch, 1, true, fa0, fb0);
+    step(fa0, fb0, ch + 1, 0, ch + 1 < C::NCH, fa1, fb1);
+  }
+}
+
+__global__ __launch_bounds__(512, 1)
+void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
+                    const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
+                    const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
+  using C = Conv2Cfg;
+  using L = Conv12P;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool producer = wave >= 4;
+  const int ptid = tid - 256;
+  const int ntiles = 2 * nimg;
+  const int T = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile_of = [&](int j) { return (int)blockIdx.x + j * (int)gridDim.x; };
+  uint8_t* patch0 = lds;
+  uint8_t* patch1 = lds + L::PATCH;
+  uint8_t* in8_0 = lds + L::OFF_IN;
+  uint8_t* in8_1 = lds + L::OFF_IN + Conv12::IN8_AL;
+
+  // ---- once per workgroup: resident conv2 weights (ring layout), epilogue
+  // constants of both layers, the patch column halos of both buffers
+  for (int e = tid; e < L::WRES / 16; e += 512) {
+    const int o = e * 16;
+    const int ch = o / C::WBUF, oc = o % C::WBUF;
+    const int r = oc >> 6, sl = (oc >> 4) & 3;
+    *reinterpret_cast<uint4*>(lds + L::OFF_W + o) = *reinterpret_cast<const uint4*>(
+        w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4));
+  }
+  stage_epik<64, 512>(ep1, reinterpret_cast<float*>(lds + L::OFF_EPI1), tid);
+  stage_epik<64, 512>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
+  if (tid < 16)
+    reinterpret_cast<int4*>(lds + L::OFF_CORR2)[tid] = reinterpret_cast<const int4*>(ep2.corr)[tid];
+  const uint32_t padw = xor80(splat_u8(x2_zp));
+  const uint4 pad4 = make_uint4(padw, padw, padw, padw);
+  for (int e = tid; e < 2 * C::PROWS * 8; e += 512) {
+    const int buf = e / (C::PROWS * 8), r = e % (C::PROWS * 8);
+    const int pr = r / 8, pc = ((r / 4) & 1) ? C::PCOLS - 1 : 0, chunk = r & 3;
+    *reinterpret_cast<uint4*>(lds + buf * L::PATCH + C::slot(0, pr, pc) + chunk * 16) = pad4;
+  }
+
+  float xv[12];
+  bool xok[12];
+  // The window index math below depends only on the thread id; laundering it
+  // through an empty asm per use keeps LICM from hoisting ~40 loop-invariant
+  // values out of the tile loop (they were spilled: the consumer's MFMA state
+  // shares the register budget).
+  auto fresh_ptid = [&]() {
+    int v = ptid;
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  // Window staging, vectorised: producer thread pt < 180 owns window row
+  // rr = pt / 9 and columns 4g-2 .. 4g+1 (g = pt % 9) of all three channels:
+  // three 16-B loads (8-B aligned: dword-aligned is enough) and one 12-byte
+  // [col][c] run in LDS.  Out-of-image rows/columns quantize to in_zp.
+  auto stage_load = [&](int t) {
+    const int n = t >> 1, y0 = (t & 1) * 16;
+    const int pt = fresh_ptid();
+    const int rr = pt / 9, g = pt % 9;
+    const int iy = y0 - 2 + rr, c0 = 4 * g - 2;
+    const bool row_ok = pt < 180 && iy >= 0 && iy < 32;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      // columns c0..c0+3 lie in [0, 32) except for g = 0 (c0 = -2) and g = 8 (c0 = 30):
+      // load from a clamped in-row start and select per element
+      const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
+      const float4 v = row_ok ? *reinterpret_cast<const float4*>(x + (((long)n * 3 + c) * 32 + iy) * 32 + cl)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = c0 + e;          // wanted column
+        const int idx = col - cl;        // its position in the loaded 4 (if inside)
+        xv[c * 4 + e] = (idx == 0) ? vv[0] : (idx == 1) ? vv[1] : (idx == 2) ? vv[2] : vv[3];
+        xok[c * 4 + e] = row_ok && col >= 0 && col < 32;
+      }
+    }
+  };
+  auto stage_store = [&](uint8_t* in8) {  // quantize (aten quantize_per_tensor) -> s8
+    const int pt = fresh_ptid();
+    if (pt < 180) {
+      const int rr = pt / 9, g = pt % 9;
+      uint32_t wd[3] = {0, 0, 0};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          int q = in_zp;
+          if (xok[c * 4 + e]) {
+            float t = xv[c * 4 + e] * in_inv;
+            t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
+            q = (int)__builtin_rintf(t) + in_zp;
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+          }
+          const int b = e * 3 + c;       // byte within the 12-byte [col][c] run
+          wd[b >> 2] |= (uint32_t)((q ^ 0x80) & 0xff) << (8 * (b & 3));
+        }
+      uint32_t* d = reinterpret_cast<uint32_t*>(in8 + (rr * Conv12::IN_C + 4 * g) * 3);
+      d[0] = wd[0]; d[1] = wd[1]; d[2] = wd[2];
+    }
+    if (pt < 4) in8[Conv12::IN8 + pt] = 0;  // bytes the 9-byte reader may touch
+  };
+  auto fresh = [](int v) {  // see fresh_ptid
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  bool vuni = false, muni = false;
+  const bool fast1 = epi_fast(ep1);
+  auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb) {
+    const int y0 = (t & 1) * 16;
+    const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
+    const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
+    // conv1 A operand and corrected accumulator init (per tile: keeping them
+    // live across the loop would add to the consumer's register budget)
+    v4i a1[2];
+    v16i c1[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a1[i] = *reinterpret_cast<const v4i*>(w1 + (i * 32 + l32) * 32 + hi * 16);
+      c1[i] = acc_init_corr(ep1.corr, i * 32, hi);
+    }
+    auto bop = [&](int tr) {
+      uint32_t r0a, r0b, r0c, r1a, r1b, r1c, r2a, r2b, r2c;
+      lds_bytes9(in8, ((tr + 0) * Conv12::IN_C + l32 + 1) * 3, r0a, r0b, r0c);
+      lds_bytes9(in8, ((tr + 1) * Conv12::IN_C + l32 + 1) * 3, r1a, r1b, r1c);
+      lds_bytes9(in8, ((tr + 2) * Conv12::IN_C + l32 + 1) * 3, r2a, r2b, r2c);
+      v4i b;
+      if (hi == 0) {  // k 0..15 = row0[0..9) + row1[0..7)
+        b = (v4i){(int)r0a, (int)r0b, (int)(r0c | (r1a << 8)), (int)((r1a >> 24) | (r1b << 8))};
+      } else {        // k 16..31 = row1[7..9) + row2[0..9) + 5 zero bytes
+        b = (v4i){(int)((r1b >> 24) | (r1c << 8) | (r2a << 16)), (int)((r2a >> 16) | (r2b << 16)),
+                  (int)((r2b >> 16) | (r2c << 16)), 0};
+      }
+      return b;
+    };
+    auto rows = [&](auto mode) {
+      constexpr int MODE = decltype(mode)::value;  // 0 general, 1 v+mult uniform, 2 v uniform
+      // lean epilogue constants: u (and mult unless uniform) of this lane's
+      // 16 channels per half; v (and mult) as scalars.  EpiK (96 VGPRs) for
+      // the general path only.
+      float u[2][16], m[2][16];
+      const float sv = ek1[64], sm = ek1[128];
+      if constexpr (MODE != 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int co = i * 32 + 8 * g + 4 * hi;
+            const float4 u4 = *reinterpret_cast<const float4*>(ek1 + co);
+            u[i][4 * g] = u4.x; u[i][4 * g + 1] = u4.y; u[i][4 * g + 2] = u4.z; u[i][4 * g + 3] = u4.w;
+            if constexpr (MODE == 2) {
+              const float4 m4 = *reinterpret_cast<const float4*>(ek1 + 128 + co);
+              m[i][4 * g] = m4.x; m[i][4 * g + 1] = m4.y; m[i][4 * g + 2] = m4.z; m[i][4 * g + 3] = m4.w;
+            }
+          }
+      }
+      for (int tr = wave - 4; tr < 18; tr += 4) {
+        const int iy = y0 - 1 + tr;
+        uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
+        if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
+          *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
+          *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
+          continue;
+        }
+        const v4i b = bop(tr);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b, c1[i], 0, 0, 0);
+          if constexpr (MODE == 0) {
+            epilogue_tile_kf<1, true>(&acc, load_epik_lds(ek1, 64, i * 32, hi), ep1, i * 32, hi,
+                                      prow_ptr);
+          } else {
+            uint32_t w[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              uint32_t wd = 0;
+#pragma unroll
+              for (int e = 0; e < 4; e += 2) {
+                const int rg = 4 * g + e;
+                const v2f af = {(float)acc[rg], (float)acc[rg + 1]};
+                const v2f tt = __builtin_elementwise_fma((v2f){u[i][rg], u[i][rg + 1]}, (v2f){sv, sv}, af);
+                const v2f ab = tt * (MODE == 1 ? (v2f){sm, sm} : (v2f){m[i][rg], m[i][rg + 1]});
+                wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.x, e, wd);
+                wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
+              }
+              w[g] = wd;
+            }
+            auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
+            auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
+            w[0] = s01[0]; w[1] = s01[1]; w[2] = s23[0]; w[3] = s23[1];
+            auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+            auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+            w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
+            *reinterpret_cast<uint4*>(prow_ptr + i * 32 + 16 * hi) =
+                make_uint4(xor80(w[0]), xor80(w[1]), xor80(w[2]), xor80(w[3]));
+          }
+        }
+      }
+    };
+    if (fast1 && vuni) {
+      if (muni) rows(std::integral_constant<int, 1>{});
+      else rows(std::integral_constant<int, 2>{});
+    } else {
+      rows(std::integral_constant<int, 0>{});
+    }
+  };
+  auto conv2_tile = [&](int t, const uint8_t* pb) {
+    const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
+    v16i acc[2][4];
+    conv_mainloop_res<C>(pb, lds + L::OFF_W, reinterpret_cast<const int*>(lds + L::OFF_CORR2),
+                         wave, ln, acc);
+    const int n = t >> 1, h = t & 1;
+    const float* ek2 = reinterpret_cast<const float*>(lds + L::OFF_EPI2);
+    uint8_t* dst = y + ((long)n * 256 + h * 128 + wave * 32 + l32) * 64;
+#ifdef QCN_EXP_NOEPI
+    {  // keep every accumulator live (no DCE), skip the requant
+      int x = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) x ^= acc[i][j][r];
+      if (x == 0x12345678) dst[0] = 1;
+      return;
+    }
+#endif
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      epilogue_tile_kf<4>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi, dst);
+  };
+
+#ifdef QCN_STAMPS
+  unsigned long long busy = 0, pa_ = 0, pb_ = 0, t_start = __builtin_amdgcn_s_memtime();
+  if (tid == 0) qcn_stamps[blockIdx.x & 0xffff][6] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (producer && T > 0) {
+    stage_load(tile_of(0));
+    stage_store(in8_0);
+  }
+  __syncthreads();
+  // conv1 requant specialisation: v (and mult) identical across channels —
+  // per-tensor weights give v = 1/aws, mult = aws/s_y; per-channel v = 1
+  {
+    const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
+    const int l = lane;
+    vuni = __builtin_amdgcn_ballot_w64(ek1[64 + l] != ek1[64]) == 0;
+    muni = __builtin_amdgcn_ballot_w64(ek1[128 + l] != ek1[128]) == 0;
+  }
+#ifdef QCN_STAMPS
+  const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
+#endif
+  for (int j = 0; j <= T; ++j) {
+#ifdef QCN_STAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (producer) {
+#ifndef QCN_EXP_NOPROD
+      if (j + 1 < T) stage_load(tile_of(j + 1));
+#ifdef QCN_STAMPS
+      const unsigned long long ta_ = __builtin_amdgcn_s_memtime();
+      pa_ += ta_ - t0;
+#endif
+      if (j < T) conv1_tile(tile_of(j), (j & 1) ? in8_1 : in8_0, (j & 1) ? patch1 : patch0);
+#ifdef QCN_STAMPS
+      const unsigned long long tb_ = __builtin_amdgcn_s_memtime();
+      pb_ += tb_ - ta_;
+#endif
+      if (j + 1 < T) stage_store(((j + 1) & 1) ? in8_1 : in8_0);
+#endif
+    } else if (j >= 1) {
+#ifndef QCN_EXP_NOCONS
+      conv2_tile(tile_of(j - 1), ((j - 1) & 1) ? patch1 : patch0);
+#endif
+    }
+#ifdef QCN_STAMPS
+    busy += __builtin_amdgcn_s_memtime() - t0;
+#endif
+    __syncthreads();
+  }
+#ifdef QCN_STAMPS
+  // [0] start, [1] +prologue, [2] +consumer busy (wave 0), [3] +producer busy (wave 4), [5] end
+  if (tid == 0) {
+    qcn_stamps[blockIdx.x & 0xffff][0] = t_start;
+    qcn_stamps[blockIdx.x & 0xffff][1] = t_pro;
+    qcn_stamps[blockIdx.x & 0xffff][2] = t_pro + busy;
+  }
+  __syncthreads();
+  if (tid == 256) {
+    qcn_stamps[blockIdx.x & 0xffff][3] = qcn_stamps[blockIdx.x & 0xffff][2] + busy;
+    qcn_stamps[(blockIdx.x + 4096) & 0xffff][0] = pa_;   // producer: stage_load issue
+    qcn_stamps[(blockIdx.x + 4096) & 0xffff][1] = pb_;   // producer: conv1
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned long long e = __builtin_amdgcn_s_memtime();
+    qcn_stamps[blockIdx.x & 0xffff][4] = qcn_stamps[blockIdx.x & 0xffff][3];
+    qcn_stamps[blockIdx.x & 0xffff][5] = e > qcn_stamps[blockIdx.x & 0xffff][4] ? e : qcn_stamps[blockIdx.x & 0xffff][4];
+    qcn_stamps[blockIdx.x & 0xffff][7] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // --------------------------------------------------------------------------
@@ -943,14 +1321,18 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   if (qdq1) { ep1.qdq = 1; ep1.s1 = qdq1->s1; ep1.z1 = qdq1->z1; ep1.inv2 = qdq1->inv2; ep1.z2 = qdq1->z2; }
   ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0};
   if (qdq2) { ep2.qdq = 1; ep2.s1 = qdq2->s1; ep2.z1 = qdq2->z1; ep2.inv2 = qdq2->inv2; ep2.z2 = qdq2->z2; }
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (hipFuncSetAttribute((const void*)qcn::conv12_fused_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, qcn::Conv12::LDS) != hipSuccess)
+  static int ncu = 0;
+  if (!ncu) {
+    if (hipFuncSetAttribute((const void*)qcn::conv12p_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, qcn::Conv12P::LDS) != hipSuccess)
       return QCN_ERR_HIP;
-    attr_done = true;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      return QCN_ERR_HIP;
   }
-  hipLaunchKernelGGL(qcn::conv12_fused_kernel, dim3(nimg * 2), dim3(256), qcn::Conv12::LDS,
+  const int grid = 2 * nimg < ncu ? 2 * nimg : ncu;   // persistent: one workgroup per CU
+  hipLaunchKernelGGL(qcn::conv12p_kernel, dim3(grid), dim3(512), qcn::Conv12P::LDS,
                      (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
                      w2_packed, ep2, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;

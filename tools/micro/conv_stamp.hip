@@ -11,59 +11,41 @@
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
-static void run(int cin, int cout, int hw, int pool, int nimg) {
-  const long nin = (long)nimg * hw * hw * cin;
-  const int oh = pool ? hw / 2 : hw;
-  const long nout = (long)nimg * oh * oh * cout;
-  std::vector<uint8_t> hx(nin);
-  std::vector<int8_t> hw8((long)cout * cin * 9), hp(9L * cin * cout);
-  std::vector<int32_t> wsum(cout), corr(cout);
-  std::vector<float> u(cout, 0.5f), v(cout, 1.0f), mult(cout, 1e-3f);
-  unsigned s = 12345;
-  for (auto& e : hx) { s = s * 1103515245u + 12345u; e = (uint8_t)(s >> 16); }
-  for (auto& e : hw8) { s = s * 1103515245u + 12345u; e = (int8_t)(s >> 16); }
-  qcn_pack_conv3x3_weight(hw8.data(), cout, cin, hp.data(), wsum.data());
-  for (int i = 0; i < cout; ++i) corr[i] = (128 - 3) * wsum[i];
-  uint8_t *dx, *dy; int8_t* dw; float *du, *dv, *dm; int* dc;
-  CK(hipMalloc(&dx, nin)); CK(hipMalloc(&dy, nout)); CK(hipMalloc(&dw, hp.size()));
-  CK(hipMalloc(&du, cout * 4)); CK(hipMalloc(&dv, cout * 4)); CK(hipMalloc(&dm, cout * 4));
-  CK(hipMalloc(&dc, cout * 4));
-  CK(hipMemcpy(dx, hx.data(), nin, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dw, hp.data(), hp.size(), hipMemcpyHostToDevice));
-  CK(hipMemcpy(du, u.data(), cout * 4, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dv, v.data(), cout * 4, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dm, mult.data(), cout * 4, hipMemcpyHostToDevice));
-  CK(hipMemcpy(dc, corr.data(), cout * 4, hipMemcpyHostToDevice));
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int i = 0; i < 20; ++i)
-    qcn_conv3x3_u8s8_nhwc(dx, nimg, hw, hw, cin, 3, dw, cout, du, dv, dm, dc, 0, 1, pool, nullptr, dy, 0);
-  CK(hipEventRecord(e0));
+template <class F>
+static void report(const char* title, double macs, F launch) {
+  hipEvent_t ev0, ev1;
+  CK(hipEventCreate(&ev0)); CK(hipEventCreate(&ev1));
+  for (int i = 0; i < 20; ++i) launch();
+  CK(hipEventRecord(ev0));
   const int iters = 50;
-  for (int i = 0; i < iters; ++i)
-    qcn_conv3x3_u8s8_nhwc(dx, nimg, hw, hw, cin, 3, dw, cout, du, dv, dm, dc, 0, 1, pool, nullptr, dy, 0);
-  CK(hipEventRecord(e1));
-  CK(hipEventSynchronize(e1));
-  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  for (int i = 0; i < iters; ++i) launch();
+  CK(hipEventRecord(ev1));
+  CK(hipEventSynchronize(ev1));
+  float ms; CK(hipEventElapsedTime(&ms, ev0, ev1));
   ms /= iters;
-  // one more launch for clean stamps
-  static unsigned long long zero[1 << 16][8];
+  static unsigned long long zero[1 << 16][8], st[1 << 16][8];
   CK(hipMemcpyToSymbol(HIP_SYMBOL(qcn_stamps), zero, sizeof(zero)));
-  qcn_conv3x3_u8s8_nhwc(dx, nimg, hw, hw, cin, 3, dw, cout, du, dv, dm, dc, 0, 1, pool, nullptr, dy, 0);
+  launch();
   CK(hipDeviceSynchronize());
-  static unsigned long long st[1 << 16][8];
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(qcn_stamps), sizeof(st)));
-  const long pxb_total = (long)nimg * hw * hw;
-  // workgroup count: derive from the config used by the dispatcher
   int nwg = 0;
-  for (int b = 0; b < (1 << 16); ++b) if (st[b][0]) nwg = b + 1;
+  for (int b = 0; b < 4096; ++b) if (st[b][0]) nwg = b + 1;
+  {
+    double a = 0, b2 = 0; int cnt = 0;
+    for (int b = 4096; b < 4096 + nwg; ++b) if (st[b][1]) { a += st[b][0]; b2 += st[b][1]; ++cnt; }
+    if (cnt) printf("  producer per WG: stage_load %.0f, conv1 %.0f cycles\n", a / cnt, b2 / cnt);
+  }
+  if (nwg == 0) {
+    printf("%s: %.2f us/launch (events), %.1f TOP/s (no stamps)\n", title, ms * 1e3,
+           2 * macs / (ms * 1e-3) / 1e12);
+    return;
+  }
   unsigned long long r0 = ~0ull, r1 = 0;
-  double pro = 0, main = 0, epi = 0, clk = 0, q1 = 0, q2 = 0, q3 = 0;
+  double ph[5] = {0, 0, 0, 0, 0}, clk = 0;
   std::vector<double> starts, ends;
   for (int b = 0; b < nwg; ++b) {
     r0 = std::min(r0, st[b][6]); r1 = std::max(r1, st[b][7]);
-    pro += st[b][1] - st[b][0]; main += st[b][2] - st[b][1]; epi += st[b][5] - st[b][2];
-    q1 += st[b][3] - st[b][2]; q2 += st[b][4] - st[b][3]; q3 += st[b][5] - st[b][4];
+    for (int k = 0; k < 5; ++k) ph[k] += (double)(st[b][k + 1] - st[b][k]);
     clk += (double)(st[b][5] - st[b][0]) / ((double)(st[b][7] - st[b][6]) * 10.0);
   }
   clk /= nwg;
@@ -74,24 +56,77 @@ static void run(int cin, int cout, int hw, int pool, int nimg) {
   std::sort(starts.begin(), starts.end());
   std::sort(ends.begin(), ends.end());
   const double rspan = (double)(r1 - r0) * 10.0;  // ns
-  const double macs = (double)pxb_total * cout * cin * 9;
   const double mfma_cyc = macs / 32768.0 * 32.0 / 1024.0;  // per SIMD at 32 cyc/MFMA
-  printf("conv %d->%d @%d pool=%d  n=%d: %.2f us/launch (events), %.1f TOP/s; nwg=%d\n", cin, cout, hw,
-         pool, nimg, ms * 1e3, 2 * macs / (ms * 1e-3) / 1e12, nwg);
-  printf("  stamped launch: first start -> last end %.2f us; WG clock %.2f GHz; ideal MFMA cyc/SIMD %.0f = %.2f us\n",
+  printf("%s: %.2f us/launch (events), %.1f TOP/s; nwg=%d\n", title, ms * 1e3,
+         2 * macs / (ms * 1e-3) / 1e12, nwg);
+  printf("  stamped launch: %.2f us; WG clock %.2f GHz; ideal MFMA cyc/SIMD %.0f = %.2f us\n",
          rspan / 1e3, clk, mfma_cyc, mfma_cyc / clk / 1e3);
-  printf("  per-WG avg cycles: prologue %.0f  mainloop %.0f  epilogue %.0f (requant+stage %.0f, sync %.0f, store %.0f)\n",
-         pro / nwg, main / nwg, epi / nwg, q1 / nwg, q2 / nwg, q3 / nwg);
+  printf("  per-WG avg cycles: stage %.0f | pre-mfma %.0f | mainloop %.0f | requant+stage+sync %.0f | store %.0f\n",
+         ph[0] / nwg, ph[1] / nwg, ph[2] / nwg, ph[3] / nwg, ph[4] / nwg);
   printf("  WG start (ns) pct 0/25/50/75/90/100: %.0f %.0f %.0f %.0f %.0f %.0f\n", starts[0],
          starts[nwg / 4], starts[nwg / 2], starts[3 * nwg / 4], starts[9 * nwg / 10], starts[nwg - 1]);
   printf("  WG end   (ns) pct 0/25/50/75/90/100: %.0f %.0f %.0f %.0f %.0f %.0f\n", ends[0],
          ends[nwg / 4], ends[nwg / 2], ends[3 * nwg / 4], ends[9 * nwg / 10], ends[nwg - 1]);
+}
+
+static unsigned rng = 12345;
+static int8_t r8() { rng = rng * 1103515245u + 12345u; return (int8_t)(rng >> 16); }
+
+template <class T>
+static T* up(const std::vector<T>& h) {
+  T* d; CK(hipMalloc(&d, h.size() * sizeof(T)));
+  CK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+static void run(int cin, int cout, int hw, int pool, int nimg) {
+  const long nin = (long)nimg * hw * hw * cin;
+  const int oh = pool ? hw / 2 : hw;
+  const long nout = (long)nimg * oh * oh * cout;
+  std::vector<uint8_t> hx(nin);
+  std::vector<int8_t> hw8((long)cout * cin * 9), hp(9L * cin * cout);
+  std::vector<int32_t> wsum(cout), corr(cout);
+  for (auto& e : hx) e = (uint8_t)r8();
+  for (auto& e : hw8) e = r8();
+  qcn_pack_conv3x3_weight(hw8.data(), cout, cin, hp.data(), wsum.data());
+  for (int i = 0; i < cout; ++i) corr[i] = (128 - 3) * wsum[i];
+  uint8_t* dx = up(hx); int8_t* dw = up(hp); int* dc = up(corr);
+  float* du = up(std::vector<float>(cout, 0.5f)); float* dv = up(std::vector<float>(cout, 1.0f));
+  float* dm = up(std::vector<float>(cout, 1e-3f));
+  uint8_t* dy; CK(hipMalloc(&dy, nout));
+  char title[128];
+  snprintf(title, sizeof title, "conv %d->%d @%d pool=%d n=%d", cin, cout, hw, pool, nimg);
+  report(title, (double)nimg * hw * hw * cout * cin * 9, [&] {
+    qcn_conv3x3_u8s8_nhwc(dx, nimg, hw, hw, cin, 3, dw, cout, du, dv, dm, dc, 0, 1, pool, nullptr, dy, 0);
+  });
   CK(hipFree(dx)); CK(hipFree(dy)); CK(hipFree(dw)); CK(hipFree(du)); CK(hipFree(dv));
   CK(hipFree(dm)); CK(hipFree(dc));
 }
 
+static void run12(int nimg) {
+  std::vector<float> hx((long)nimg * 3 * 32 * 32);
+  for (auto& e : hx) e = r8() / 64.0f;
+  std::vector<int8_t> w1((long)64 * 27), w1p(64 * 32), w2(64L * 64 * 9), w2p(64L * 64 * 9);
+  for (auto& e : w1) e = r8();
+  for (auto& e : w2) e = r8();
+  std::vector<int32_t> s1(64), s2(64), c1(64), c2(64);
+  qcn_pack_conv1_weight(w1.data(), 64, w1p.data(), s1.data());
+  qcn_pack_conv3x3_weight(w2.data(), 64, 64, w2p.data(), s2.data());
+  for (int i = 0; i < 64; ++i) { c1[i] = (128 - 7) * s1[i]; c2[i] = 128 * s2[i]; }
+  float* dx = up(hx); int8_t* dw1 = up(w1p); int8_t* dw2 = up(w2p);
+  int* dc1 = up(c1); int* dc2 = up(c2);
+  float* du = up(std::vector<float>(64, 0.5f)); float* dv = up(std::vector<float>(64, 1.0f));
+  float* dm = up(std::vector<float>(64, 1e-3f));
+  uint8_t* dy; CK(hipMalloc(&dy, (long)nimg * 16 * 16 * 64));
+  report("conv12 fused (3->64->64 @32, pool)", (double)nimg * 1024 * 64 * (27 + 576), [&] {
+    qcn_conv12_fused_f32_nchw(dx, nimg, 0.05f, 7, dw1, du, dv, dm, dc1, 0, 1, nullptr, 0, dw2, du, dv,
+                              dm, dc2, 0, 1, nullptr, dy, 0);
+  });
+}
+
 int main() {
   const int n = 1024;
+  run12(n);
   run(64, 128, 16, 0, n);   // conv3
   run(128, 128, 16, 1, n);  // conv4
   run(128, 256, 8, 0, n);   // conv5
