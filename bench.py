@@ -42,6 +42,7 @@ MAC_PER_IMAGE = {"conv1": 1_769_472, "conv2": 37_748_736, "conv3": 18_874_368,
                  "conv4": 37_748_736, "conv5": 18_874_368, "conv6": 37_748_736,
                  "fc1": 2_097_152, "fc2": 5_120}
 MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
+MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -50,7 +51,8 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv5": 8 * 8 * 128 + 8 * 8 * 256,
                    "conv6": 8 * 8 * 256 + 4 * 4 * 256,
                    "fc1": 4096 + 512, "fc2": 512 + 10 + 40,
-                 "conv12": 3 * 32 * 32 * 4 + 16 * 16 * 64}
+                 "conv12": 3 * 32 * 32 * 4 + 16 * 16 * 64,
+                 "fc12": 4096 + 512 + 10 + 40}
 HBM_BOUND = {"conv1"}
 
 

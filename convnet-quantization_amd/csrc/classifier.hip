@@ -1,0 +1,210 @@
+// Classifier head of the static int8 SimpleConvNet (baseline_model.py:38-40,
+// QuantizedLinearReLU fc1 -> QuantizedLinear fc2 -> DeQuantStub), in two
+// launches instead of two full GEMM kernels:
+//
+//  1. fc_splitk_kernel: fc1's u8 x s8 GEMM (M = batch, K = 4096, N = 512) split
+//     four ways along K.  A workgroup owns a 128 (rows) x 64 (features) tile of
+//     one K quarter; its four waves each compute 64 x 32 with
+//     v_mfma_i32_32x32x32_i8 straight from global memory.  Both operands are
+//     chunk-major ([K/32][rows][32]: conv6 writes its output that way, the
+//     weights are packed so at upload), so every fragment load is one
+//     contiguous 1 KB — row-major operands (4 KB row stride) ran 2-3x slower.
+//     Tiles are numbered XCD-major: the 32 workgroups of one XCD share one
+//     128-row block of X in that XCD's L2.  int32 partial sums go to a
+//     workspace (4 x M x 512 x 4 B = 8 MB at batch 1024).
+//  2. fc_finish_kernel: one wave per row sums the partials, adds the
+//     zero-point correction, requantizes fc1 (+ReLU), writes the u8 fc1 row,
+//     then computes fc2 (512 -> n2 <= 16) from the row it holds in registers
+//     (exact integer dot products, wave reduction), requantizes and
+//     dequantizes the logits.  Numerics are those of linear_u8s8_kernel (A9).
+#include "common.hpp"
+#include "qconvnet_abi.hpp"
+
+namespace qcn {
+
+constexpr int FC_S = 4;      // K split
+constexpr int FC_N1 = 512;   // fc1 features handled by the finisher (64 lanes x 8)
+constexpr int FC_N2 = 16;    // max fc2 outputs
+
+// X' [K/32][m][32], W' [K/32][n][32] (chunk-major: a 32-row MFMA fragment of
+// one 32-byte K chunk is one contiguous 1 KB, every wave-load fully coalesced).
+__global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restrict__ x, int m, int k,
+                                                        const int8_t* __restrict__ w, int n,
+                                                        int* __restrict__ part) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int MB = m / 128, NB = n / 64, T = MB * NB * FC_S;
+  int t = blockIdx.x;
+  if (T % 8 == 0) t = (t % 8) * (T / 8) + t / 8;   // XCD-major tile order
+  const int mb = t / (NB * FC_S), rem = t % (NB * FC_S), nb = rem / FC_S, s = rem % FC_S;
+  const int mi = wave & 1, ni = wave >> 1;
+  const int row0 = mb * 128 + mi * 64, col0 = nb * 64 + ni * 32;
+  const int kcs = (k / 32) / FC_S, kc0 = s * kcs;
+  // fragment lane (l32, hi): row l32, bytes [16 hi, 16 hi + 16) of the chunk
+  const int frag = (lane & 31) * 32 + (lane >> 5) * 16;
+  const uint8_t* xa = x + ((long)kc0 * m + row0) * 32 + frag;
+  const int8_t* wa = w + ((long)kc0 * n + col0) * 32 + frag;
+  const long xs = (long)m * 32, ws = (long)n * 32;   // bytes per K chunk
+
+  v16i acc0 = (v16i){0}, acc1 = (v16i){0};
+  constexpr int U = 4;   // chunks per batch; two batches in flight
+  v4i fw[2][U];
+  uint4 f0[2][U], f1[2][U];
+  auto load = [&](int buf, int c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      fw[buf][u] = *reinterpret_cast<const v4i*>(wa + (c + u) * ws);
+      f0[buf][u] = *reinterpret_cast<const uint4*>(xa + (c + u) * xs);
+      f1[buf][u] = *reinterpret_cast<const uint4*>(xa + (c + u) * xs + 1024);
+    }
+  };
+  auto mm = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 a = f0[buf][u], b = f1[buf][u];
+      const v4i b0 = (v4i){(int)xor80(a.x), (int)xor80(a.y), (int)xor80(a.z), (int)xor80(a.w)};
+      const v4i b1 = (v4i){(int)xor80(b.x), (int)xor80(b.y), (int)xor80(b.z), (int)xor80(b.w)};
+      acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b1, acc1, 0, 0, 0);
+    }
+  };
+  load(0, 0);
+  for (int c = 0; c < kcs; c += 2 * U) {
+    if (c + U < kcs) load(1, c + U);
+    mm(0);
+    if (c + 2 * U < kcs) load(0, c + 2 * U);
+    if (c + U < kcs) mm(1);
+  }
+  // D[feature][row]: lane (l32 = row, hi) holds features 8g + 4hi + e
+  const int l32 = lane & 31, hi = lane >> 5;
+  int* pp = part + (long)s * m * n + col0 + 4 * hi;
+  const int r = row0 + l32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    *reinterpret_cast<int4*>(pp + (long)r * n + 8 * g) =
+        make_int4(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
+    *reinterpret_cast<int4*>(pp + (long)(r + 32) * n + 8 * g) =
+        make_int4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+  }
+}
+
+struct FcHead {
+  const float *u1, *v1, *m1;
+  const int* corr1;     // (128 - zx1) * wsum1 (the GEMM saw q ^ 0x80)
+  int z1, lo1;          // fc1 output zero point = fc2 input zero point
+  const int8_t* w2;
+  int n2;
+  const float *u2, *v2, *m2;
+  int z2, lo2;
+  float y2_scale;
+};
+
+__global__ __launch_bounds__(256) void fc_finish_kernel(const int* __restrict__ part, int m,
+                                                        FcHead hd, uint8_t* __restrict__ y1,
+                                                        uint8_t* __restrict__ y2,
+                                                        float* __restrict__ y2f) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= m) return;
+  const int f0 = lane * 8;
+  // every load up front (one wave per row: nothing else hides their latency)
+  int4 pv[FC_S][2];
+#pragma unroll
+  for (int s = 0; s < FC_S; ++s) {
+    const int* p = part + ((long)s * m + row) * FC_N1 + f0;
+    pv[s][0] = *reinterpret_cast<const int4*>(p);
+    pv[s][1] = *reinterpret_cast<const int4*>(p + 4);
+  }
+  const int4 c0 = *reinterpret_cast<const int4*>(hd.corr1 + f0), c1 = *reinterpret_cast<const int4*>(hd.corr1 + f0 + 4);
+  const float4 u0 = *reinterpret_cast<const float4*>(hd.u1 + f0), u4 = *reinterpret_cast<const float4*>(hd.u1 + f0 + 4);
+  const float4 v0 = *reinterpret_cast<const float4*>(hd.v1 + f0), v4 = *reinterpret_cast<const float4*>(hd.v1 + f0 + 4);
+  const float4 m0 = *reinterpret_cast<const float4*>(hd.m1 + f0), m4 = *reinterpret_cast<const float4*>(hd.m1 + f0 + 4);
+  uint2 wv[FC_N2];
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o)
+    wv[o] = *reinterpret_cast<const uint2*>(hd.w2 + (long)(o < hd.n2 ? o : 0) * FC_N1 + f0);
+
+  int a[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+  for (int s = 0; s < FC_S; ++s) {
+    a[0] += pv[s][0].x; a[1] += pv[s][0].y; a[2] += pv[s][0].z; a[3] += pv[s][0].w;
+    a[4] += pv[s][1].x; a[5] += pv[s][1].y; a[6] += pv[s][1].z; a[7] += pv[s][1].w;
+  }
+  const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u4.x, u4.y, u4.z, u4.w};
+  const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v4.x, v4.y, v4.z, v4.w};
+  const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m4.x, m4.y, m4.z, m4.w};
+  int q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) q[e] = requant_one(a[e], uu[e], vv[e], mm[e], hd.z1, hd.lo1);
+  const uint32_t lo = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  const uint32_t hw = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
+  *reinterpret_cast<uint2*>(y1 + (long)row * FC_N1 + f0) = make_uint2(lo, hw);
+
+  // fc2: exact sum_k (q1 - z1) * w2[o][k] over this lane's 8 k, for all
+  // outputs at once, then the wave reductions interleaved (independent chains)
+  int sacc[FC_N2];
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) {
+    sacc[o] = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int wb = (int)(int8_t)(((e < 4 ? wv[o].x : wv[o].y) >> (8 * (e & 3))) & 0xff);
+      sacc[o] += (q[e] - hd.z1) * wb;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int o = 0; o < FC_N2; ++o) sacc[o] += __shfl_xor(sacc[o], off);
+  int mine = 0;
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o)
+    if (lane == o) mine = sacc[o];
+  if (lane < hd.n2) {
+    const int o = lane;
+    const int q2 = requant_one(mine, hd.u2[o], hd.v2[o], hd.m2[o], hd.z2, hd.lo2);
+    y2[(long)row * hd.n2 + o] = (uint8_t)q2;
+    y2f[(long)row * hd.n2 + o] = (float)(q2 - hd.z2) * hd.y2_scale;
+  }
+}
+
+}  // namespace qcn
+
+extern "C" {
+
+int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out) {
+  if (!w || !out || n <= 0 || k <= 0 || k % 32 != 0) return QCN_ERR_ARG;
+  for (int o = 0; o < n; ++o)
+    for (int kk = 0; kk < k; ++kk)
+      out[((long)(kk / 32) * n + o) * 32 + kk % 32] = w[(long)o * k + kk];
+  return QCN_OK;
+}
+
+long long qcn_classifier_workspace_size(int m, int n1) {
+  if (m <= 0 || n1 <= 0) return 0;
+  return (long long)qcn::FC_S * m * n1 * 4;
+}
+
+int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1, const float* u1,
+                        const float* v1, const float* mult1, const int32_t* corr1, int y1_zp,
+                        int relu1, const int8_t* w2, int n2, const float* u2, const float* v2,
+                        const float* mult2, int y2_zp, int relu2, float y2_scale, void* workspace,
+                        uint8_t* y1, uint8_t* y2, float* y2f, void* stream) {
+  if (!x || !w1 || !u1 || !v1 || !mult1 || !corr1 || !w2 || !u2 || !v2 || !mult2 || !workspace ||
+      !y1 || !y2 || !y2f)
+    return QCN_ERR_ARG;
+  if (m <= 0 || k <= 0 || n1 <= 0 || n2 <= 0 || y1_zp < 0 || y1_zp > 255 || y2_zp < 0 || y2_zp > 255)
+    return QCN_ERR_ARG;
+  if (m % 128 != 0 || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 || n2 > qcn::FC_N2)
+    return QCN_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  int* part = static_cast<int*>(workspace);
+  const int tiles = (m / 128) * (n1 / 64) * qcn::FC_S;
+  hipLaunchKernelGGL(qcn::fc_splitk_kernel, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
+  qcn::FcHead hd{u1, v1, mult1, corr1, y1_zp, relu1 ? y1_zp : 0, w2, n2, u2, v2, mult2,
+                 y2_zp, relu2 ? y2_zp : 0, y2_scale};
+  hipLaunchKernelGGL(qcn::fc_finish_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd, y1,
+                     y2, y2f);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+}  // extern "C"

@@ -97,6 +97,7 @@ struct ConvEpi {
   int zp_y, lo;        // output zero point, lower clamp (zp_y if relu else 0)
   int qdq;             // 0: write requantized u8; 1: apply qdq_next
   float s1; int z1; float inv2; int z2;
+  int kmajor;          // 1: write y as [f / 32][image][32] (f = NHWC flatten index)
 };
 
 // Requantize one 32(cout) x 32(pixel) accumulator tile (optionally the max of
@@ -434,6 +435,25 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
   QCN_STAMP(4);
   const long out0 = (long)blockIdx.x * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
+  if (ep.kmajor) {
+    // chunk-major for the classifier GEMM: 32-byte chunk kc of image n at
+    // y + (kc * nimg + n) * 32.  The workgroup holds whole images, so the
+    // IMGS images of one chunk form one contiguous run (IMGS * 32 bytes).
+    constexpr int OPI = POOL ? C::IMG / 4 : C::IMG;   // output pixels per image
+    constexpr int IMGS = C::OPX / OPI;
+    if constexpr (IMGS >= 1 && C::OPX % OPI == 0) {
+      constexpr int CC = COUT / 32;
+      const int n0 = (int)(out0 / OPI);
+      for (int e = tid; e < OPI * CC * IMGS * 2; e += C::NT) {
+        const int half = e & 1, img = (e >> 1) % IMGS, pc = (e >> 1) / IMGS;
+        const int p = pc / CC, cc = pc % CC;
+        if (n0 + img < nimg)
+          *reinterpret_cast<uint4*>(y + ((long)(p * CC + cc) * nimg + n0 + img) * 32 + half * 16) =
+              *reinterpret_cast<const uint4*>(lout + (img * OPI + p) * C::OS + cc * 32 + half * 16);
+      }
+    }
+    return;
+  }
   store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
 }
 
@@ -1278,6 +1298,20 @@ int qcn_pack_conv1_weight(const int8_t* w_oihw, int cout, int8_t* out, int32_t* 
   return QCN_OK;
 }
 
+int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                            const int8_t* w_packed, int cout, const float* u, const float* v,
+                            const float* mult, const int32_t* corr, int y_zp, int relu, int pool,
+                            uint8_t* y, void* stream) {
+  if (!x || !w_packed || !u || !v || !mult || !corr || !y) return QCN_ERR_ARG;
+  if (nimg <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return QCN_ERR_ARG;
+  if (x_zp < 0 || x_zp > 255 || y_zp < 0 || y_zp > 255) return QCN_ERR_ARG;
+  if (pool && ((h & 1) || (w & 1))) return QCN_ERR_ARG;
+  // whole images per workgroup: the 8x8 -> 4x4 and 8x8 layers of the net
+  if (!(h == 8 && w == 8 && cin % 64 == 0 && cout == 256)) return QCN_ERR_UNSUPPORTED;
+  ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 1};
+  return dispatch_conv(cin, cout, h, pool, x, nimg, x_zp, w_packed, ep, y, (hipStream_t)stream);
+}
+
 int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
                           const int8_t* w_packed, int cout, const float* u, const float* v,
                           const float* mult, const int32_t* corr, int y_zp, int relu, int pool,
@@ -1286,7 +1320,7 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
   if (nimg <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return QCN_ERR_ARG;
   if (x_zp < 0 || x_zp > 255 || y_zp < 0 || y_zp > 255) return QCN_ERR_ARG;
   if (pool && ((h & 1) || (w & 1))) return QCN_ERR_ARG;
-  ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0};
+  ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
   if (qdq) {
     ep.qdq = 1;
     ep.s1 = qdq->s1; ep.z1 = qdq->z1; ep.inv2 = qdq->inv2; ep.z2 = qdq->z2;
@@ -1317,9 +1351,9 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f) || x2_zp < 0 || x2_zp > 255 ||
       y_zp < 0 || y_zp > 255 || z1 < 0 || z1 > 255)
     return QCN_ERR_ARG;
-  ConvEpi ep1{u1, v1, mult1, corr1, z1, relu1 ? z1 : 0, 0, 0.f, 0, 0.f, 0};
+  ConvEpi ep1{u1, v1, mult1, corr1, z1, relu1 ? z1 : 0, 0, 0.f, 0, 0.f, 0, 0};
   if (qdq1) { ep1.qdq = 1; ep1.s1 = qdq1->s1; ep1.z1 = qdq1->z1; ep1.inv2 = qdq1->inv2; ep1.z2 = qdq1->z2; }
-  ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0};
+  ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
   if (qdq2) { ep2.qdq = 1; ep2.s1 = qdq2->s1; ep2.z1 = qdq2->z1; ep2.inv2 = qdq2->inv2; ep2.z2 = qdq2->z2; }
   static int ncu = 0;
   if (!ncu) {
@@ -1344,7 +1378,7 @@ int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_
                        uint8_t* q_in, void* stream) {
   if (!x || !w1_packed || !u || !v || !mult || !corr || !y) return QCN_ERR_ARG;
   if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
-  ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0};
+  ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
   if (qdq) {
     ep.qdq = 1;
     ep.s1 = qdq->s1; ep.z1 = qdq->z1; ep.inv2 = qdq->inv2; ep.z2 = qdq->z2;

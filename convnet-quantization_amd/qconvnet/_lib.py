@@ -54,6 +54,12 @@ SIGNATURES = {
                                         C.POINTER(QDQ), i32, vp, vp, vp, vp, vp, i32, i32,
                                         C.POINTER(QDQ), vp, vp]),
     "qcn_linear_u8s8": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, f32, vp]),
+    "qcn_classifier_workspace_size": (i64, [i32, i32]),
+    "qcn_pack_fc_kmajor": (i32, [vp, i32, i32, vp]),
+    "qcn_conv3x3_u8s8_kmajor": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
+                                      i32, vp, vp]),
+    "qcn_classifier_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp,
+                                  vp, i32, i32, f32, vp, vp, vp, vp, vp]),
     "qcn_linear_dynamic_workspace_size": (i64, [i32, i32]),
     "qcn_linear_dynamic_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp]),
     "qcn_linear_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp]),

@@ -185,6 +185,64 @@ def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=F
     return (out, out_f) if want_fp32 else out
 
 
+def classifier_workspace(m, n1, device):
+    return torch.empty(lib().qcn_classifier_workspace_size(m, n1), dtype=torch.uint8, device=device)
+
+
+def pack_fc_kmajor(w: np.ndarray):
+    """s8 [n, k] -> chunk-major [k/32, n, 32] (the classifier head's fc1 layout)."""
+    w = np.ascontiguousarray(w, dtype=np.int8)
+    n, k = w.shape
+    out = np.empty((k // 32, n, 32), np.int8)
+    check(lib().qcn_pack_fc_kmajor(w.ctypes.data, n, k, out.ctypes.data), "pack_fc_kmajor")
+    return out
+
+
+def to_kmajor(x2d):
+    """u8 [m, k] -> chunk-major [k/32, m, 32] (torch; tests and fallbacks)."""
+    m, k = x2d.shape
+    return x2d.view(m, k // 32, 32).permute(1, 0, 2).contiguous()
+
+
+def from_kmajor(xk):
+    """chunk-major [k/32, m, 32] -> [m, k]."""
+    kc, m, _ = xk.shape
+    return xk.permute(1, 0, 2).reshape(m, kc * 32)
+
+
+def conv3x3_kmajor(x, x_zp, w_packed, cout, u, v, mult, corr, y_zp, relu, pool, out):
+    """conv3x3 whose output is chunk-major [oh*ow*cout/32, n, 32] (conv6 -> fc1).
+    Returns False when the shape is not supported (caller uses conv3x3)."""
+    _need(x, torch.uint8, "conv_kmajor.x")
+    n, h, w, cin = x.shape
+    rc = lib().qcn_conv3x3_u8s8_kmajor(_ptr(x), n, h, w, cin, int(x_zp), _ptr(w_packed), cout,
+                                       _ptr(u), _ptr(v), _ptr(mult), _ptr(corr), int(y_zp),
+                                       int(bool(relu)), int(bool(pool)), _ptr(out), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "conv3x3_kmajor")
+    return True
+
+
+def classifier(xk, l1, l2, workspace, y1, y2, y2f):
+    """Static fc1(+ReLU) -> fc2 -> dequantize head (two launches).  ``xk`` is the
+    chunk-major fc1 input [k/32, m, 32]; ``l1``/``l2`` carry wk (chunk-major fc1
+    weights) / w, u, v, mult, (l1) corr, z_y, relu and (l2) s_y.  Returns False
+    when the shape is outside the kernel's envelope (caller falls back)."""
+    _need(xk, torch.uint8, "classifier.x")
+    kc, m, _ = xk.shape
+    k = kc * 32
+    rc = lib().qcn_classifier_u8s8(_ptr(xk), m, k, _ptr(l1.wk), l1.wk.shape[1], _ptr(l1.u), _ptr(l1.v),
+                                   _ptr(l1.mult), _ptr(l1.corr), int(l1.z_y), int(bool(l1.relu)),
+                                   _ptr(l2.w), l2.w.shape[0], _ptr(l2.u), _ptr(l2.v), _ptr(l2.mult),
+                                   int(l2.z_y), int(bool(l2.relu)), float(l2.s_y), _ptr(workspace),
+                                   _ptr(y1), _ptr(y2), _ptr(y2f), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "classifier")
+    return True
+
+
 def linear_dynamic(x, w, w_scale, wsum, bias, reduce_range=True, workspace=None, out=None):
     """quantized::linear_dynamic on the device (fp32 in, fp32 out)."""
     _need(x, torch.float32, "linear_dynamic.x")

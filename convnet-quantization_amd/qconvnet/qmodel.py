@@ -23,6 +23,8 @@ plus torch.ao prepare/convert with MinMax observers (observer.py:349-427).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -256,6 +258,8 @@ class QuantizedConvNet:
             wsum = w.astype(np.int64).sum(1)
             u, v, mult = Q.epilogue_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
             d.w = self._t(w)
+            if name == "fc1" and w.shape[1] % 32 == 0:
+                d.wk = self._t(ops.pack_fc_kmajor(w))   # classifier-head layout
             d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
             d.corr = self._t(((128 - int(e["z_x"])) * wsum).astype(np.int32))
             d.z_x, d.z_y, d.s_y, d.relu = int(e["z_x"]), int(e["z_y"]), F32(e["s_y"]), e["relu"]
@@ -284,8 +288,20 @@ class QuantizedConvNet:
 
     def kernel_names(self, x_shape):
         """Names of the launches run() marks, in order (conv1+conv2 are one
-        launch when fused)."""
-        return self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS
+        launch when fused; fc1+fc2 one "fc12" slot for the fused head)."""
+        names = self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS
+        if self._head_fused(x_shape[0]):
+            names = names[:-2] + ("fc12",)
+        return names
+
+    def _head_fused(self, n):
+        f1, f2 = self.fc1, self.fc2
+        if os.environ.get("QCN_FC_HEAD", "fused") == "linear":   # A/B switch (tools/ab.sh)
+            return False
+        c6 = self.L[5]
+        return (self.mode == "static" and n % 128 == 0 and f1.w.shape[0] == 512 and
+                f1.w.shape[1] == 4096 and hasattr(f1, "wk") and f2.w.shape[0] <= 16 and
+                f2.z_x == f1.z_y and c6.qdq is None and c6.cout == 256 and c6.pool)
 
     def _fused(self, x_shape):
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
@@ -318,21 +334,36 @@ class QuantizedConvNet:
                           d.relu, d.qdq, out=b["a1"])
             mark()
             prev, first = b["a1"], 1
+        head = self._head_fused(n)
         for i in range(first, 6):
             d = L[i]
+            if i == 5 and head:   # conv6 writes the classifier's chunk-major input
+                if "a6k" not in b:
+                    b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
+                if not ops.conv3x3_kmajor(prev, d.z_x, d.w, d.cout, d.u, d.v, d.mult, d.corr,
+                                          d.z_y, d.relu, d.pool, b["a6k"]):
+                    raise RuntimeError("chunk-major conv6 rejected a supported shape")
+                mark()
+                continue
             ops.conv3x3(prev, d.z_x, d.w, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, d.pool,
                         d.qdq, out=b[names[i - 1]])
             mark()
             prev = b[names[i - 1]]
-        flat = prev.view(n, 4096)
         f1, f2 = self.fc1, self.fc2
-        if self.mode == "static":
+        if head:
+            if not self._classifier(b["a6k"], b):
+                raise RuntimeError("classifier head rejected a supported shape")
+            if keep:  # NHWC view of conv6's output for inspection / parity tests
+                b["a6"].copy_(ops.from_kmajor(b["a6k"]).view(n, 4, 4, 256))
+        elif self.mode == "static":
+            flat = prev.view(n, 4096)
             ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, True,
                           out=b["f1"])
             mark()
             ops.linear_u8(b["f1"], f2.z_x, f2.w, f2.u, f2.v, f2.mult, f2.corr, f2.z_y, False,
                           y_scale=f2.s_y, want_fp32=True, out=b["q"], out_f=b["logits"])
         else:
+            flat = prev.view(n, 4096)
             ops.linear_u8(flat, f1.z_x, f1.w, f1.u, f1.v, f1.mult, f1.corr, f1.z_y, False,
                           y_scale=f1.s_y, want_fp32=True, out=b["f1"], out_f=b["f1f"])
             mark()
@@ -341,6 +372,16 @@ class QuantizedConvNet:
         if keep:
             return b["logits"], b
         return b["logits"]
+
+    def _classifier(self, xk, b):
+        """fc1+ReLU -> fc2 -> dequantize in two launches (split-K fc1 on the
+        chunk-major conv6 output + a per-row finisher)."""
+        f1, f2 = self.fc1, self.fc2
+        n = xk.shape[1]
+        if "ws" not in b:
+            b["ws"] = ops.classifier_workspace(n, f1.w.shape[0], self.device)
+        f1.relu, f2.relu = True, False
+        return ops.classifier(xk, f1, f2, b["ws"], b["f1"], b["q"], b["logits"])
 
     def capture_graph(self, x_static):
         """Capture run(x_static) into a HIP graph; replay with replay(n)."""

@@ -115,6 +115,15 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
                               const int32_t* corr2, int y_zp, int relu2, const qcn_qdq_t* qdq2,
                               uint8_t* y, void* stream);
 
+/* A5/A6 as above, but y is written chunk-major for the classifier head:
+ * y[f / 32][nimg][32] with f the NHWC flatten index of one image's output
+ * (oh * ow * cout bytes).  Supported: the 8x8 layers with cout == 256
+ * (SimpleConvNet conv5/conv6), QCN_ERR_UNSUPPORTED otherwise. */
+int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                            const int8_t* w_packed, int cout, const float* u, const float* v,
+                            const float* mult, const int32_t* corr, int y_zp, int relu, int pool,
+                            uint8_t* y, void* stream);
+
 /* A9 — quantized Linear / LinearReLU (fbgemm), static qparams:
  * fc1/fc2 of SimpleConvNet (baseline_model.py:38,40).
  *   x: u8 [m,k] (zero point x_zp); w: s8 [n,k] row-major; y: u8 [m,n].
@@ -122,6 +131,26 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
 int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, int n,
                     const float* u, const float* v, const float* mult, const int32_t* corr,
                     int y_zp, int relu, uint8_t* y, float* y_deq, float y_scale, void* stream);
+
+/* A9 x 2 + A7 — the static classifier head in two launches: fc1 (+ReLU)
+ * u8 x s8 -> u8 [m, n1] as a 4-way split-K GEMM into an int32 workspace, then
+ * one wave per row finishes fc1 (requant) and computes fc2 (n2 <= 64) and its
+ * DeQuantStub.  Same results as qcn_linear_u8s8(fc1) followed by
+ * qcn_linear_u8s8(fc2, y_deq) — fc2's input zero point is y1_zp, fc2's
+ * correction is applied exactly in the finisher (no corr2 argument).
+ * x and w1 are CHUNK-MAJOR: x[k/32][m][32] (qcn_conv3x3_u8s8_kmajor writes
+ * conv6's output that way), w1[k/32][n1][32] (qcn_pack_fc_kmajor).
+ * corr1 = (128 - x_zp) * sum_k w1[f][k].  Supported: m % 128 == 0, n1 == 512,
+ * k % 1024 == 0, n2 <= 16 (QCN_ERR_UNSUPPORTED otherwise).  workspace: device
+ * memory of qcn_classifier_workspace_size(m, n1) bytes. */
+long long qcn_classifier_workspace_size(int m, int n1);
+/* Host: s8 [n][k] row-major -> [k/32][n][32] (k % 32 == 0). */
+int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out);
+int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1, const float* u1,
+                        const float* v1, const float* mult1, const int32_t* corr1, int y1_zp,
+                        int relu1, const int8_t* w2, int n2, const float* u2, const float* v2,
+                        const float* mult2, int y2_zp, int relu2, float y2_scale, void* workspace,
+                        uint8_t* y1, uint8_t* y2, float* y2_deq, void* stream);
 
 /* A8 — quantized::linear_dynamic (DynamicQuantizedLinear of
  * models/static_ptq_model.py:28-32 and models/dynamic_ptq_model.py:302-306):

@@ -284,3 +284,72 @@ def test_fused_conv12_equals_unfused(dev, mode):
     b = QuantizedConvNet(spec, dev, fuse12=True).run(x, keep=True)[1]["a2"].clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("per_channel,zx,z1,z2", [(False, 0, 0, 131), (True, 17, 0, 90),
+                                                   (False, 200, 40, 7)])
+def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
+    """Split-K fc1 on chunk-major operands + fused fc1-finish/fc2
+    (qcn_classifier_u8s8) == the two
+    static linear kernels (which match fbgemm: test_linear_golden), bit for
+    bit on u8 fc1, u8 logits and fp32 logits.  Also the oracle for fc1."""
+    from types import SimpleNamespace as NS
+    from qconvnet import ops, quant as Q
+    rng = np.random.default_rng(7 + zx)
+    m, k, n1, n2 = 256, 4096, 512, 10
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    qx = rng.integers(0, 256, (m, k), dtype=np.uint8)
+    w1 = rng.integers(-128, 128, (n1, k), dtype=np.int8)
+    w2 = rng.integers(-128, 128, (n2, n1), dtype=np.int8)
+    s_x, s_y1, s_y2 = F32(0.02), F32(0.05), F32(0.11)
+    s_w1 = (rng.uniform(1e-4, 3e-4, n1).astype(F32) if per_channel else F32(2e-4))
+    s_w2 = (rng.uniform(1e-3, 3e-3, n2).astype(F32) if per_channel else F32(2e-3))
+    b1 = rng.normal(0, 0.5, n1).astype(F32)
+    b2 = rng.normal(0, 0.5, n2).astype(F32)
+    u1, v1, m1 = Q.epilogue_constants(s_x, s_w1, s_y1, b1)
+    u2, v2, m2 = Q.epilogue_constants(s_y1, s_w2, s_y2, b2)
+    corr1 = ((128 - zx) * w1.astype(np.int64).sum(1)).astype(np.int32)
+    corr2 = ((128 - z1) * w2.astype(np.int64).sum(1)).astype(np.int32)
+    y1_ref = ops.linear_u8(T(qx), zx, T(w1), T(u1), T(v1), T(m1), T(corr1), z1, True)
+    y2_ref, y2f_ref = ops.linear_u8(y1_ref, z1, T(w2), T(u2), T(v2), T(m2), T(corr2), z2, False,
+                                    y_scale=s_y2, want_fp32=True)
+    l1 = NS(w=T(w1), wk=T(ops.pack_fc_kmajor(w1)), u=T(u1), v=T(v1), mult=T(m1), corr=T(corr1),
+            z_y=z1, relu=True)
+    l2 = NS(w=T(w2), u=T(u2), v=T(v2), mult=T(m2), z_y=z2, relu=False, s_y=s_y2)
+    ws = ops.classifier_workspace(m, n1, dev)
+    y1 = torch.empty((m, n1), dtype=torch.uint8, device=dev)
+    y2 = torch.empty((m, n2), dtype=torch.uint8, device=dev)
+    y2f = torch.empty((m, n2), dtype=torch.float32, device=dev)
+    assert ops.classifier(ops.to_kmajor(T(qx)), l1, l2, ws, y1, y2, y2f)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y1_ref)
+    assert torch.equal(y2, y2_ref)
+    assert torch.equal(y2f, y2f_ref)
+    # fc1 against the numpy oracle on a slice (A9 numerics)
+    want = qref.linear_q(qx[:32], zx, w1, u1, v1, m1, z1, True)
+    assert np.array_equal(y1[:32].cpu().numpy(), want)
+    # outside the envelope -> QCN_ERR_UNSUPPORTED -> False (caller falls back)
+    assert not ops.classifier(ops.to_kmajor(T(qx[:100])), l1, l2, ws, y1, y2, y2f)
+
+
+@pytest.mark.parametrize("pool", [True, False])
+def test_conv_kmajor_output(dev, pool):
+    """qcn_conv3x3_u8s8_kmajor writes exactly the NHWC result, chunk-major."""
+    from qconvnet import ops
+    rng = np.random.default_rng(3)
+    n, hw, cin, cout = 12, 8, 256, 256
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    qx = rng.integers(0, 256, (n, hw, hw, cin), dtype=np.uint8)
+    w = rng.integers(-128, 128, (cout, cin, 3, 3), dtype=np.int8)
+    packed, wsum = ops.pack_conv3x3(w)
+    u = rng.normal(0, 1, cout).astype(F32)
+    v = np.full(cout, F32(1e-3), F32)
+    mult = np.full(cout, F32(3e-3), F32)
+    corr = ((128 - 9) * wsum.astype(np.int64)).astype(np.int32)
+    args = (9, T(packed), cout, T(u), T(v), T(mult), T(corr), 0, True, pool)
+    ref = ops.conv3x3(T(qx), *args)
+    oh = hw // 2 if pool else hw
+    out = torch.empty((oh * oh * cout // 32, n, 32), dtype=torch.uint8, device=dev)
+    assert ops.conv3x3_kmajor(T(qx), *args, out)
+    torch.cuda.synchronize()
+    assert torch.equal(ops.from_kmajor(out), ref.view(n, -1))
