@@ -631,143 +631,7 @@ void conv1_f32_kernel(const float* __restrict__ x, int nimg, float in_inv, int i
   store_staged<64, 80, 256>(lout, 512, y + p0 * 64, total - p0, tid);
 }
 
-// --------------------------------------------------------------------------
-// conv1 + conv2 fused (SimpleConvNet block 1: QuantStub -> conv1+ReLU ->
-// conv2+ReLU -> 2x2 max-pool).  conv1's 64-channel output never reaches HBM:
-// each workgroup (16 output rows of one 32x32 image, 4 waves) recomputes conv1
-// for the 18 x 32 positions conv2's 3x3 window needs (1.125x conv1 work, which
-// is 4.7 % of conv2's) straight into conv2's LDS input patch, then runs the
-// shared conv2 main loop.  Saves the 64 MB write + 64 MB read of the
-// activation at batch 1024.  Numerics are those of the unfused pair.
 using Conv2Cfg = ConvCfg<64, 64, 32, true, 4, 16, 96, 0, true>;
-struct Conv12 {
-  static constexpr int IN_R = 20, IN_C = 36;                 // fp32 input window
-  static constexpr int IN8 = IN_R * IN_C * 3;                 // s8 [row][col][c]
-  static constexpr int IN8_AL = (IN8 + 4 + 15) / 16 * 16;     // +4: over-read guard
-  static constexpr int SCRATCH0 = IN8_AL;                     // phase 0-2
-  static constexpr int SCRATCH1 = 3 * Conv2Cfg::WBUF;         // phase 3 (weight ring)
-  static constexpr int MAIN = Conv2Cfg::PATCH + (SCRATCH0 > SCRATCH1 ? SCRATCH0 : SCRATCH1);
-  // conv_epilogue reads conv2's constants at Conv2Cfg::EPI
-  static_assert(Conv2Cfg::EPI >= MAIN, "epilogue constants outside the scratch");
-  static constexpr int LDS = Conv2Cfg::LDS;
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
-};
-
-// 9 consecutive bytes of LDS at byte offset off (any alignment) as
-// (bytes 0-3, bytes 4-7, byte 8): three dword reads + v_alignbyte.
-QCN_DEV void lds_bytes9(const uint8_t* base, int off, uint32_t& w0, uint32_t& w1, uint32_t& b8) {
-  const uint32_t* d = reinterpret_cast<const uint32_t*>(base + (off & ~3));
-  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3];
-  const uint32_t sh = (off & 3) * 8;
-  w0 = sh ? ((d0 >> sh) | (d1 << (32 - sh))) : d0;
-  w1 = sh ? ((d1 >> sh) | (d2 << (32 - sh))) : d1;
-  const uint32_t w2 = sh ? ((d2 >> sh) | (d3 << (32 - sh))) : d2;
-  b8 = w2 & 0xff;
-}
-
-__global__ __launch_bounds__(256, 2)
-void conv12_fused_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
-                         const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
-                         const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
-  using C = Conv2Cfg;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* patch = lds;
-  uint8_t* in8 = lds + C::PATCH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l32 = lane & 31, hi = lane >> 5;
-  const int n = blockIdx.x >> 1;
-  const int y0 = (blockIdx.x & 1) * 16;
-  QCN_STAMP(0);
-
-  // phase 0: quantized input window (rows y0-2..y0+17, cols -2..33, [row][col][c])
-  // with unconditional batched loads, and conv2's patch halo = its input zp
-  {
-    constexpr int NITER = (Conv12::IN8 + 255) / 256;   // 9
-    float v[NITER];
-    bool ok[NITER];
-#pragma unroll
-    for (int k = 0; k < NITER; ++k) {
-      const int it = tid + k * 256;
-      const int itc = it < Conv12::IN8 ? it : 0;
-      const int c = itc / (Conv12::IN_R * Conv12::IN_C);
-      const int rr = (itc / Conv12::IN_C) % Conv12::IN_R, cc = itc % Conv12::IN_C;
-      const int iy = y0 - 2 + rr, ix = cc - 2;
-      ok[k] = iy >= 0 && iy < 32 && ix >= 0 && ix < 32;
-      v[k] = x[ok[k] ? (((long)n * 3 + c) * 32 + iy) * 32 + ix : 0];
-    }
-#pragma unroll
-    for (int k = 0; k < NITER; ++k) {
-      const int it = tid + k * 256;
-      if (it >= Conv12::IN8) continue;
-      const int c = it / (Conv12::IN_R * Conv12::IN_C);
-      const int rr = (it / Conv12::IN_C) % Conv12::IN_R, cc = it % Conv12::IN_C;
-      int q = in_zp;
-      if (ok[k]) {
-        float t = v[k] * in_inv;
-        t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
-        q = (int)__builtin_rintf(t) + in_zp;
-        q = q < 0 ? 0 : (q > 255 ? 255 : q);
-      }
-      in8[(rr * Conv12::IN_C + cc) * 3 + c] = (uint8_t)(q ^ 0x80);
-    }
-    if (tid < 4) in8[Conv12::IN8 + tid] = 0;  // bytes the 9-byte reader may touch
-  }
-  stage_epik<64, 256>(ep2, reinterpret_cast<float*>(lds + C::EPI), tid);
-  const uint32_t padw = xor80(splat_u8(x2_zp));
-  const uint4 pad4 = make_uint4(padw, padw, padw, padw);
-  for (int it = tid; it < C::PROWS * C::PCOLS * 4; it += 256) {
-    const int sl = it >> 2, chunk = it & 3;
-    const int pr = sl / C::PCOLS, pc = sl % C::PCOLS;
-    const int iy = y0 + pr - 1;
-    if (iy < 0 || iy >= 32 || pc == 0 || pc == C::PCOLS - 1)
-      *reinterpret_cast<uint4*>(patch + C::slot(0, pr, pc) + chunk * 16) = pad4;
-  }
-  __syncthreads();
-
-  QCN_STAMP(1);
-  // phase 1+2: conv1 on MFMA, one 32-pixel row tile (patch row t) per step.
-  // Each lane builds its own B operand (pixel l32, k half hi) from the three
-  // 9-byte input runs (k = r*9 + s*3 + c), then the epilogue writes the
-  // requantized row straight into conv2's patch (as q - 128).
-  v4i a1[2];
-  v16i c1[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    a1[i] = *reinterpret_cast<const v4i*>(w1 + (i * 32 + l32) * 32 + hi * 16);
-    c1[i] = acc_init_corr(ep1.corr, i * 32, hi);
-  }
-  const EpiK k1a = load_epik(ep1, 0, hi), k1b = load_epik(ep1, 32, hi);
-  for (int t = wave; t < 18; t += 4) {
-    const int iy = y0 - 1 + t;
-    if (iy < 0 || iy >= 32) continue;  // wave-uniform: halo row keeps the pad value
-    uint32_t r0a, r0b, r0c, r1a, r1b, r1c, r2a, r2b, r2c;
-    lds_bytes9(in8, ((t + 0) * Conv12::IN_C + l32 + 1) * 3, r0a, r0b, r0c);
-    lds_bytes9(in8, ((t + 1) * Conv12::IN_C + l32 + 1) * 3, r1a, r1b, r1c);
-    lds_bytes9(in8, ((t + 2) * Conv12::IN_C + l32 + 1) * 3, r2a, r2b, r2c);
-    v4i b;
-    if (hi == 0) {  // k 0..15 = row0[0..9) + row1[0..7)
-      b = (v4i){(int)r0a, (int)r0b, (int)(r0c | (r1a << 8)), (int)((r1a >> 24) | (r1b << 8))};
-    } else {        // k 16..31 = row1[7..9) + row2[0..9) + 5 zero bytes
-      b = (v4i){(int)((r1b >> 24) | (r1c << 8) | (r2a << 16)), (int)((r2a >> 16) | (r2b << 16)),
-                (int)((r2b >> 16) | (r2c << 16)), 0};
-    }
-    uint8_t* prow_ptr = patch + C::slot(0, t, l32 + 1);
-    const v16i acc1a = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[0], b, c1[0], 0, 0, 0);
-    const v16i acc1b = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[1], b, c1[1], 0, 0, 0);
-    epilogue_tile_kf<1, true>(&acc1a, k1a, ep1, 0, hi, prow_ptr);
-    epilogue_tile_kf<1, true>(&acc1b, k1b, ep1, 32, hi, prow_ptr);
-  }
-
-  // phase 3: conv2 (main loop issues its weight ring over the input window,
-  // which every wave must have finished reading)
-  __syncthreads();
-  QCN_STAMP(2);
-  v16i acc[2][4];
-  conv_mainloop<C>(patch, lds + C::PATCH, w2, ep2.corr, wave, lane, acc);
-  QCN_STAMP(3);
-  conv_epilogue<C>(acc, ep2, lds, nimg, wave, lane, tid, y);
-  QCN_STAMP(5);
-}
 
 // --------------------------------------------------------------------------
 // conv1 + conv2 fused, persistent and wave-specialised (the production path).
@@ -785,9 +649,13 @@ struct Conv12P {
   using C = Conv2Cfg;
   static constexpr int PATCH = C::PATCH;
   static constexpr int WRES = 9 * C::WBUF;                 // all conv2 weights
+  // quantized fp32 input window: rows y0-2..y0+17, cols -2..33, one dword per
+  // pixel (c0, c1, c2, 0) so conv1's im2col operand is plain aligned dwords
+  static constexpr int IN_R = 20, IN_C = 36;
+  static constexpr int IN8 = IN_R * IN_C * 4;
   static constexpr int OFF_W = 2 * PATCH;
   static constexpr int OFF_IN = OFF_W + WRES;              // 2 x quantized input window
-  static constexpr int OFF_EPI1 = OFF_IN + 2 * Conv12::IN8_AL;
+  static constexpr int OFF_EPI1 = OFF_IN + 2 * IN8;
   static constexpr int OFF_EPI2 = OFF_EPI1 + 12 * 64;
   static constexpr int OFF_CORR2 = OFF_EPI2 + 12 * 64;      // conv2 corr (int32 x 64)
   static constexpr int LDS = OFF_CORR2 + 4 * 64;
@@ -864,7 +732,7 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
   uint8_t* patch0 = lds;
   uint8_t* patch1 = lds + L::PATCH;
   uint8_t* in8_0 = lds + L::OFF_IN;
-  uint8_t* in8_1 = lds + L::OFF_IN + Conv12::IN8_AL;
+  uint8_t* in8_1 = lds + L::OFF_IN + L::IN8;
 
   // ---- once per workgroup: resident conv2 weights (ring layout), epilogue
   // constants of both layers, the patch column halos of both buffers
@@ -929,9 +797,10 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
     const int pt = fresh_ptid();
     if (pt < 180) {
       const int rr = pt / 9, g = pt % 9;
-      uint32_t wd[3] = {0, 0, 0};
+      uint32_t wd[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < 4; ++e) {
+        uint32_t d = 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           int q = in_zp;
@@ -941,13 +810,12 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
             q = (int)__builtin_rintf(t) + in_zp;
             q = q < 0 ? 0 : (q > 255 ? 255 : q);
           }
-          const int b = e * 3 + c;       // byte within the 12-byte [col][c] run
-          wd[b >> 2] |= (uint32_t)((q ^ 0x80) & 0xff) << (8 * (b & 3));
+          d |= (uint32_t)((q ^ 0x80) & 0xff) << (8 * c);
         }
-      uint32_t* d = reinterpret_cast<uint32_t*>(in8 + (rr * Conv12::IN_C + 4 * g) * 3);
-      d[0] = wd[0]; d[1] = wd[1]; d[2] = wd[2];
+        wd[e] = d;
+      }
+      *reinterpret_cast<uint4*>(in8 + (rr * L::IN_C + 4 * g) * 4) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
-    if (pt < 4) in8[Conv12::IN8 + pt] = 0;  // bytes the 9-byte reader may touch
   };
   auto fresh = [](int v) {  // see fresh_ptid
     asm volatile("" : "+v"(v));
@@ -959,28 +827,41 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
     const int y0 = (t & 1) * 16;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
     const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
-    // conv1 A operand and corrected accumulator init (per tile: keeping them
-    // live across the loop would add to the consumer's register budget)
-    v4i a1[2];
+    // conv1 A operand in the dword-per-tap K order: step 0 covers taps 0..7
+    // (k' = 4 tap + c, c = 3 -> 0), step 1 tap 8; rebuilt per tile from the
+    // [64][32] (k = 3 tap + c) packing, and the corrected accumulator init
+    // (per tile: keeping them live across the loop would add to the consumer's
+    // register budget)
+    v4i a1[2][2];
     v16i c1[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      a1[i] = *reinterpret_cast<const v4i*>(w1 + (i * 32 + l32) * 32 + hi * 16);
+      const uint4 r0 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32);
+      const uint4 r1 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32 + 16);
+      const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      auto byte = [&](int k) -> uint32_t { return (wd[k >> 2] >> (8 * (k & 3))) & 0xff; };
+      auto tapw = [&](int t) -> int {   // (w[3t], w[3t+1], w[3t+2], 0)
+        return (int)(byte(3 * t) | (byte(3 * t + 1) << 8) | (byte(3 * t + 2) << 16));
+      };
+      // constant byte indices (a lane-dependent index would put wd[] in scratch)
+      const v4i lo4 = (v4i){tapw(0), tapw(1), tapw(2), tapw(3)};
+      const v4i hi4 = (v4i){tapw(4), tapw(5), tapw(6), tapw(7)};
+      a1[i][0] = hi ? hi4 : lo4;
+      a1[i][1] = (v4i){hi ? 0 : tapw(8), 0, 0, 0};
       c1[i] = acc_init_corr(ep1.corr, i * 32, hi);
     }
-    auto bop = [&](int tr) {
-      uint32_t r0a, r0b, r0c, r1a, r1b, r1c, r2a, r2b, r2c;
-      lds_bytes9(in8, ((tr + 0) * Conv12::IN_C + l32 + 1) * 3, r0a, r0b, r0c);
-      lds_bytes9(in8, ((tr + 1) * Conv12::IN_C + l32 + 1) * 3, r1a, r1b, r1c);
-      lds_bytes9(in8, ((tr + 2) * Conv12::IN_C + l32 + 1) * 3, r2a, r2b, r2c);
-      v4i b;
-      if (hi == 0) {  // k 0..15 = row0[0..9) + row1[0..7)
-        b = (v4i){(int)r0a, (int)r0b, (int)(r0c | (r1a << 8)), (int)((r1a >> 24) | (r1b << 8))};
-      } else {        // k 16..31 = row1[7..9) + row2[0..9) + 5 zero bytes
-        b = (v4i){(int)((r1b >> 24) | (r1c << 8) | (r2a << 16)), (int)((r2a >> 16) | (r2b << 16)),
-                  (int)((r2b >> 16) | (r2c << 16)), 0};
+    const int* in32 = reinterpret_cast<const int*>(in8);
+    auto bop = [&](int tr, v4i& b0, v4i& b1) {
+      const int* r0 = in32 + (tr + 0) * L::IN_C + l32 + 1;   // input cols l32-1 .. l32+1
+      const int* r1 = r0 + L::IN_C;
+      const int* r2 = r1 + L::IN_C;
+      if (hi == 0) {   // taps (0,0) (0,1) (0,2) (1,0) | (2,2)
+        b0 = (v4i){r0[0], r0[1], r0[2], r1[0]};
+        b1 = (v4i){r2[2], 0, 0, 0};
+      } else {         // taps (1,1) (1,2) (2,0) (2,1)
+        b0 = (v4i){r1[1], r1[2], r2[0], r2[1]};
+        b1 = (v4i){0, 0, 0, 0};
       }
-      return b;
     };
     auto rows = [&](auto mode) {
       constexpr int MODE = decltype(mode)::value;  // 0 general, 1 v+mult uniform, 2 v uniform
@@ -1011,10 +892,12 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
           *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
           continue;
         }
-        const v4i b = bop(tr);
+        v4i b0, b1;
+        bop(tr, b0, b1);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b, c1[i], 0, 0, 0);
+          v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc, 0, 0, 0);
           if constexpr (MODE == 0) {
             epilogue_tile_kf<1, true>(&acc, load_epik_lds(ek1, 64, i * 32, hi), ep1, i * 32, hi,
                                       prow_ptr);
