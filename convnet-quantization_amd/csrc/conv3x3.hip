@@ -824,6 +824,9 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
   bool vuni = false, muni = false;
   const bool fast1 = epi_fast(ep1);
   auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb) {
+    // producer waves issue first: their VALU-bound conv1 is the longer phase,
+    // the consumer's MFMAs fill the gaps (measured 53.6 vs 59.2 us)
+    __builtin_amdgcn_s_setprio(2);
     const int y0 = (t & 1) * 16;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
     const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
@@ -884,47 +887,85 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
             }
           }
       }
-      for (int tr = wave - 4; tr < 18; tr += 4) {
-        const int iy = y0 - 1 + tr;
-        uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
-        if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
-          *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
-          *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
-          continue;
-        }
-        v4i b0, b1;
-        bop(tr, b0, b1);
+      if constexpr (MODE == 0) {
+        for (int tr = wave - 4; tr < 18; tr += 4) {
+          const int iy = y0 - 1 + tr;
+          uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
+          if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
+            *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
+            *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
+            continue;
+          }
+          v4i b0, b1;
+          bop(tr, b0, b1);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc, 0, 0, 0);
-          if constexpr (MODE == 0) {
+          for (int i = 0; i < 2; ++i) {
+            v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc, 0, 0, 0);
             epilogue_tile_kf<1, true>(&acc, load_epik_lds(ek1, 64, i * 32, hi), ep1, i * 32, hi,
                                       prow_ptr);
-          } else {
-            uint32_t w[4];
+          }
+        }
+      } else {
+        // rows w, w+4, ... of this producer wave, software-pipelined: the next
+        // row's im2col reads and MFMAs are issued before this row's requant,
+        // so the VALU never waits on an MFMA result (that cost ~40 s_nop per
+        // row).  Halo rows are computed like the others and then overwritten.
+        const int w = wave - 4;
+        const int nr = w < 2 ? 5 : 4;
+        auto mfma_row = [&](int tr, v16i (&acc)[2]) {
+          v4i b0, b1;
+          bop(tr, b0, b1);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc[i], 0, 0, 0);
+          }
+        };
+        v16i acc_n[2];
+        mfma_row(w, acc_n);
+        for (int kr = 0; kr < nr; ++kr) {
+          const int tr = w + 4 * kr;
+          v16i acc[2] = {acc_n[0], acc_n[1]};
+          if (kr + 1 < nr) mfma_row(tr + 4, acc_n);
+          // requant both 32-channel halves in stages (independent pairs
+          // interleave instead of a dependent fma -> mul -> cvt chain per pair)
+          v2f t[2][8];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int pr = 0; pr < 8; ++pr)
+              t[i][pr] = (v2f){(float)acc[i][2 * pr], (float)acc[i][2 * pr + 1]};
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int pr = 0; pr < 8; ++pr)
+              t[i][pr] = __builtin_elementwise_fma((v2f){u[i][2 * pr], u[i][2 * pr + 1]}, (v2f){sv, sv},
+                                                   t[i][pr]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int pr = 0; pr < 8; ++pr)
+              t[i][pr] = t[i][pr] * (MODE == 1 ? (v2f){sm, sm} : (v2f){m[i][2 * pr], m[i][2 * pr + 1]});
+          uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
+          // the lane's 4-channel groups 8g + 4hi go straight to their dwords in
+          // the patch row (v_permlane32_swap costs ~25 cycles each,
+          // tools/micro/valu_rate.hip; four ds_write_b32 are cheaper)
+          uint32_t* pdw = reinterpret_cast<uint32_t*>(prow_ptr) + hi;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              uint32_t wd = 0;
-#pragma unroll
-              for (int e = 0; e < 4; e += 2) {
-                const int rg = 4 * g + e;
-                const v2f af = {(float)acc[rg], (float)acc[rg + 1]};
-                const v2f tt = __builtin_elementwise_fma((v2f){u[i][rg], u[i][rg + 1]}, (v2f){sv, sv}, af);
-                const v2f ab = tt * (MODE == 1 ? (v2f){sm, sm} : (v2f){m[i][rg], m[i][rg + 1]});
-                wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.x, e, wd);
-                wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
-              }
-              w[g] = wd;
+              uint32_t wd = __builtin_amdgcn_cvt_pk_u8_f32(t[i][2 * g].x, 0, 0u);
+              wd = __builtin_amdgcn_cvt_pk_u8_f32(t[i][2 * g].y, 1, wd);
+              wd = __builtin_amdgcn_cvt_pk_u8_f32(t[i][2 * g + 1].x, 2, wd);
+              wd = __builtin_amdgcn_cvt_pk_u8_f32(t[i][2 * g + 1].y, 3, wd);
+              pdw[i * 8 + 2 * g] = xor80(wd);   // channels i*32 + 8g + 4hi .. +3
             }
-            auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
-            auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
-            w[0] = s01[0]; w[1] = s01[1]; w[2] = s23[0]; w[3] = s23[1];
-            auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
-            auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
-            w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
-            *reinterpret_cast<uint4*>(prow_ptr + i * 32 + 16 * hi) =
-                make_uint4(xor80(w[0]), xor80(w[1]), xor80(w[2]), xor80(w[3]));
+          const int iy = y0 - 1 + tr;
+          if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
+            *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
+            *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
           }
         }
       }

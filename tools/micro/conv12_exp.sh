@@ -1,7 +1,7 @@
 # conv12 producer/consumer isolation timings (diagnostic builds; outputs wrong by design)
 set -e
-for V in "" "-DQCN_EXP_NOPROD" "-DQCN_EXP_NOCONS"; do
+for V in "" "-DQCN_EXP_PRIOP=2" "-DQCN_EXP_NOCONS" "-DQCN_EXP_NOPROD"; do
   echo "=== variant: $V"
   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -DQCN_STAMPS $V -Iinclude -Iconvnet-quantization_amd/csrc tools/micro/conv_stamp.hip -o /tmp/conv_stamp_x
-  timeout -k 10 60 /tmp/conv_stamp_x
+  timeout -k 10 60 /tmp/conv_stamp_x | head -3
 done
