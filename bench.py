@@ -43,6 +43,8 @@ MAC_PER_IMAGE = {"conv1": 1_769_472, "conv2": 37_748_736, "conv3": 18_874_368,
                  "fc1": 2_097_152, "fc2": 5_120}
 MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
 MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
+MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
+MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -52,7 +54,9 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv6": 8 * 8 * 256 + 4 * 4 * 256,
                    "fc1": 4096 + 512, "fc2": 512 + 10 + 40,
                  "conv12": 3 * 32 * 32 * 4 + 16 * 16 * 64,
-                 "fc12": 4096 + 512 + 10 + 40}
+                 "fc12": 4096 + 512 + 10 + 40,
+                 "conv34": 16 * 16 * 64 + 8 * 8 * 128,
+                 "conv56": 8 * 8 * 128 + 4 * 4 * 256}
 HBM_BOUND = {"conv1"}
 
 

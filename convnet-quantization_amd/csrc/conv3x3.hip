@@ -409,13 +409,14 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 // the workgroup's contiguous NHWC output span with 16-B stores.
 template <class C>
 QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, int nimg,
-                           int wave, int lane, int tid, uint8_t* __restrict__ y) {
+                           int wave, int lane, int tid, uint8_t* __restrict__ y,
+                           const float* ek_override = nullptr) {
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
   constexpr bool POOL = C::kPool;
   constexpr int COUT = C::kCout;
   uint8_t* lout = lds;  // the patch / weight ring is dead after the last barrier
-  const float* ek = reinterpret_cast<const float*>(lds + C::EPI);
+  const float* ek = ek_override ? ek_override : reinterpret_cast<const float*>(lds + C::EPI);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int co_base = wc * 64 + i * 32;
@@ -457,29 +458,15 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
   store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
 }
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
-__global__ __launch_bounds__(COUT * WPX, 2)
-void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                         const int8_t* __restrict__ wpk, ConvEpi ep,
-                         uint8_t* __restrict__ y) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* patch = lds;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-
-  QCN_STAMP(0);
-  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
-  const int n0 = (int)(p0 / C::IMG);
-  const int y0 = (int)((p0 % C::IMG) / C::W);
-
-  // ---- stage the input patch (q ^ 0x80 = q - 128 as s8; halo = zp ^ 0x80).
-  // Loads are issued in unconditional batches (halo / tail lanes read a valid
-  // dummy address and are replaced afterwards) so a thread keeps BATCH 16-B
-  // loads in flight instead of one dependent HBM round trip per element.
-  stage_epik<COUT, C::NT>(ep, reinterpret_cast<float*>(lds + C::EPI), tid);
+// Stage the input patch of the workgroup's tile (images n0.., first output row
+// y0) in LDS: q ^ 0x80 = q - 128 as s8, halo = zp ^ 0x80.  Loads are issued in
+// unconditional batches (halo / tail lanes read a valid dummy address and are
+// replaced afterwards) so a thread keeps BATCH 16-B loads in flight instead of
+// one dependent HBM round trip per element.
+template <class C>
+QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int n0, int y0,
+                         uint8_t* patch, int tid) {
+  constexpr int CIN = C::kCin;
   const uint32_t padw = xor80(splat_u8(x_zp));
   constexpr int CH16 = CIN / 16;
   constexpr int NSLOT = C::SEGS * C::PROWS * C::PCOLS;
@@ -512,6 +499,29 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
     }
   }
 
+}
+
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
+__global__ __launch_bounds__(COUT * WPX, 2)
+void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                         const int8_t* __restrict__ wpk, ConvEpi ep,
+                         uint8_t* __restrict__ y) {
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* patch = lds;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+
+  QCN_STAMP(0);
+  const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
+  const int n0 = (int)(p0 / C::IMG);
+  const int y0 = (int)((p0 % C::IMG) / C::W);
+
+  stage_epik<COUT, C::NT>(ep, reinterpret_cast<float*>(lds + C::EPI), tid);
+  stage_patch<C>(x, nimg, x_zp, n0, y0, patch, tid);
+
   QCN_STAMP(1);
   QCN_STAMP(2);
   v16i acc[2][4];
@@ -519,6 +529,87 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   QCN_STAMP(3);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
   QCN_STAMP(5);
+}
+
+// --------------------------------------------------------------------------
+// Two convolutions of one SimpleConvNet block in one launch: A (no pool) then
+// B (2x2 pool), e.g. conv3 -> conv4 and conv5 -> conv6.  The workgroup tile is
+// whole images for both, so A's output for the tile is exactly B's input
+// patch: A's epilogue requantizes straight into B's swizzled LDS patch (as
+// q - 128, plus B's zero-point halo) and B runs without touching HBM.  Saves
+// A's output store, B's patch load and one lockstep prologue per tile.
+template <class CA, class CB>
+struct PairCfg {
+  static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
+                CA::W == CB::W, "same whole-image tiling");
+  static constexpr int MAIN_A = CA::PATCH + 3 * CA::WBUF;
+  static constexpr int MAIN_B = CB::PATCH + 3 * CB::WBUF;
+  static constexpr int MAIN = MAIN_A > MAIN_B ? MAIN_A : MAIN_B;
+  static constexpr int OUT_B = CB::OPX * CB::OS;
+  static_assert(OUT_B <= MAIN, "B's staging fits the dead patch");
+  // A's constants are dead once A's epilogue has run: park them in B's weight
+  // ring when they fit there (B's ring is only written once B's loop starts)
+  static constexpr bool EA_IN_RING = MAIN_A + 12 * CA::kCout <= MAIN_B && MAIN_A >= CB::PATCH;
+  static constexpr int OFF_EA = EA_IN_RING ? MAIN_A : MAIN;
+  static constexpr int OFF_EB = EA_IN_RING ? MAIN : MAIN + 12 * CA::kCout;
+  static constexpr int LDS = OFF_EB + 12 * CB::kCout;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class CA, class CB>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                     const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                     const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  using P = PairCfg<CA, CB>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long p0 = (long)blockIdx.x * CA::PXB;
+  const int n0 = (int)(p0 / CA::IMG);
+  const int y0 = (int)((p0 % CA::IMG) / CA::W);
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
+  stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
+  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
+
+  v16i acc[2][4];
+  conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
+
+  // ---- A's epilogue into B's patch (A's patch and ring are dead past the
+  // main loop's final barrier): zero-point halo, then the requantized interior
+  {
+    const uint32_t padw = xor80(splat_u8(xb_zp));
+    const uint4 pad4 = make_uint4(padw, padw, padw, padw);
+    constexpr int CH16 = CB::kCin / 16;
+    constexpr int HALO = CB::SEGS * (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
+    for (int e = tid; e < HALO * CH16; e += CB::NT) {
+      const int hs = e / CH16, chunk = e % CH16;
+      const int seg = hs / (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
+      int r = hs % (2 * CB::PCOLS + 2 * (CB::PROWS - 2)), pr, pc;
+      if (r < CB::PCOLS) { pr = 0; pc = r; }
+      else if (r < 2 * CB::PCOLS) { pr = CB::PROWS - 1; pc = r - CB::PCOLS; }
+      else { r -= 2 * CB::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? CB::PCOLS - 1 : 0; }
+      *reinterpret_cast<uint4*>(lds + CB::slot(seg, pr, pc) + chunk * 16) = pad4;
+    }
+    const int wc = wave % CA::WCO, wp = wave / CA::WCO;
+    const int l32 = lane & 31, hi = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co_base = wc * 64 + i * 32;
+      const EpiK K = load_epik_lds(eka, CA::kCout, co_base, hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = (wp * 4 + j) * 32 + l32;
+        const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
+        epilogue_tile_kf<1, true>(&acc[i][j], K, epa, co_base, hi, lds + CB::slot(seg, row + 1, col + 1));
+      }
+    }
+  }
+  __syncthreads();
+  conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
+  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, ekb);
 }
 
 // --------------------------------------------------------------------------
@@ -1144,6 +1235,24 @@ int launch_conv(const uint8_t* x, int nimg, int x_zp, const int8_t* wpk, const C
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+template <class CA, class CB>
+int launch_pair(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
+                int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
+  using P = PairCfg<CA, CB>;
+  const long pix = (long)nimg * CA::IMG;
+  const int grid = (int)((pix + CA::PXB - 1) / CA::PXB);
+  auto k = convpair_kernel<CA, CB>;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS) !=
+        hipSuccess)
+      return QCN_ERR_HIP;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 // Tuned instantiations: the SimpleConvNet layers and the
 // small shapes the parity fixtures use.
 int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nimg, int x_zp,
@@ -1220,6 +1329,43 @@ int qcn_pack_conv1_weight(const int8_t* w_oihw, int cout, int8_t* out, int32_t* 
     wsum[co] = s;
   }
   return QCN_OK;
+}
+
+int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
+                          const int8_t* wa_packed, int cmid, const float* ua, const float* va,
+                          const float* multa, const int32_t* corra, int zmid, int relua,
+                          const qcn_qdq_t* qdqa, const int8_t* wb_packed, int cout, const float* ub,
+                          const float* vb, const float* multb, const int32_t* corrb, int y_zp,
+                          int relub, const qcn_qdq_t* qdqb, int kmajor, uint8_t* y, void* stream) {
+  if (!x || !wa_packed || !ua || !va || !multa || !corra || !wb_packed || !ub || !vb || !multb ||
+      !corrb || !y)
+    return QCN_ERR_ARG;
+  if (nimg <= 0 || hw <= 0 || x_zp < 0 || x_zp > 255 || zmid < 0 || zmid > 255 || y_zp < 0 ||
+      y_zp > 255)
+    return QCN_ERR_ARG;
+  ConvEpi epa{ua, va, multa, corra, zmid, relua ? zmid : 0, 0, 0.f, 0, 0.f, 0, 0};
+  int xb_zp = zmid;
+  if (qdqa) {
+    epa.qdq = 1;
+    epa.s1 = qdqa->s1; epa.z1 = qdqa->z1; epa.inv2 = qdqa->inv2; epa.z2 = qdqa->z2;
+    xb_zp = qdqa->z2;
+  }
+  ConvEpi epb{ub, vb, multb, corrb, y_zp, relub ? y_zp : 0, 0, 0.f, 0, 0.f, 0, kmajor ? 1 : 0};
+  if (qdqb) {
+    epb.qdq = 1;
+    epb.s1 = qdqb->s1; epb.z1 = qdqb->z1; epb.inv2 = qdqb->inv2; epb.z2 = qdqb->z2;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  using namespace qcn;
+  if (hw == 16 && cin == 64 && cmid == 128 && cout == 128)
+    return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
+                       ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
+        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256)
+    return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
+                       ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
+        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+  return QCN_ERR_UNSUPPORTED;
 }
 
 int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,

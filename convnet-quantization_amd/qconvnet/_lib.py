@@ -56,6 +56,9 @@ SIGNATURES = {
     "qcn_linear_u8s8": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, vp, f32, vp]),
     "qcn_classifier_workspace_size": (i64, [i32, i32]),
     "qcn_pack_fc_kmajor": (i32, [vp, i32, i32, vp]),
+    "qcn_conv3x3_pair_u8s8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
+                                    C.POINTER(QDQ), vp, i32, vp, vp, vp, vp, i32, i32,
+                                    C.POINTER(QDQ), i32, vp, vp]),
     "qcn_conv3x3_u8s8_kmajor": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
                                       i32, vp, vp]),
     "qcn_classifier_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp,

@@ -210,6 +210,24 @@ def from_kmajor(xk):
     return xk.permute(1, 0, 2).reshape(m, kc * 32)
 
 
+def conv_pair(x, la, lb, out, kmajor=False):
+    """conv A (no pool) + conv B (2x2 pool) of one block in one launch (A's
+    output stays in LDS).  ``la``/``lb`` carry w, cout, u, v, mult, corr, z_x,
+    z_y, relu, qdq.  Returns False when the block shape is not supported."""
+    _need(x, torch.uint8, "conv_pair.x")
+    n, h, w, cin = x.shape
+    rc = lib().qcn_conv3x3_pair_u8s8(
+        _ptr(x), n, h, cin, int(la.z_x), _ptr(la.w), la.cout, _ptr(la.u), _ptr(la.v), _ptr(la.mult),
+        _ptr(la.corr), int(la.z_y), int(bool(la.relu)), C.byref(la.qdq) if la.qdq is not None else None,
+        _ptr(lb.w), lb.cout, _ptr(lb.u), _ptr(lb.v), _ptr(lb.mult), _ptr(lb.corr), int(lb.z_y),
+        int(bool(lb.relu)), C.byref(lb.qdq) if lb.qdq is not None else None, int(bool(kmajor)),
+        _ptr(out), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "conv_pair")
+    return True
+
+
 def conv3x3_kmajor(x, x_zp, w_packed, cout, u, v, mult, corr, y_zp, relu, pool, out):
     """conv3x3 whose output is chunk-major [oh*ow*cout/32, n, 32] (conv6 -> fc1).
     Returns False when the shape is not supported (caller uses conv3x3)."""

@@ -210,6 +210,7 @@ class QuantizedConvNet:
         self.is_custom_quantized = self.mode == "qdq"
         self.host_io = False
         self.fuse12 = fuse12
+        self.fuse_pairs = True
         self._bufs = {}
         self._graphs = {}
         self._upload()
@@ -286,13 +287,22 @@ class QuantizedConvNet:
     KERNELS = ("conv1", "conv2", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2")
     KERNELS_FUSED = ("conv12", "conv3", "conv4", "conv5", "conv6", "fc1", "fc2")
 
-    def kernel_names(self, x_shape):
+    def kernel_names(self, x_shape, keep=False):
         """Names of the launches run() marks, in order (conv1+conv2 are one
-        launch when fused; fc1+fc2 one "fc12" slot for the fused head)."""
-        names = self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS
+        launch when fused, conv3+conv4 / conv5+conv6 one launch each when
+        paired, fc1+fc2 one "fc12" slot for the fused head)."""
+        names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
+        if self._pairs(keep):
+            names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
         if self._head_fused(x_shape[0]):
-            names = names[:-2] + ("fc12",)
-        return names
+            names = names[:-2] + ["fc12"]
+        return tuple(names)
+
+    def _pairs(self, keep):
+        """conv3+conv4 and conv5+conv6 as fused block launches (their middle
+        activation stays in LDS); keep=True runs them per layer so every
+        activation is inspectable."""
+        return self.fuse_pairs and not keep and os.environ.get("QCN_PAIRS", "1") == "1"
 
     def _head_fused(self, n):
         f1, f2 = self.fc1, self.fc2
@@ -335,8 +345,24 @@ class QuantizedConvNet:
             mark()
             prev, first = b["a1"], 1
         head = self._head_fused(n)
+        pairs = self._pairs(keep)
         for i in range(first, 6):
             d = L[i]
+            if pairs and i in (2, 4):   # conv3+conv4, conv5+conv6 in one launch each
+                nb = L[i + 1]
+                if i == 4 and head:
+                    if "a6k" not in b:
+                        b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
+                    out, km = b["a6k"], True
+                else:
+                    out, km = b[names[i]], False
+                if not ops.conv_pair(prev, d, nb, out, kmajor=km):
+                    raise RuntimeError("fused conv pair rejected a supported shape")
+                mark()
+                prev = out
+                continue
+            if pairs and i in (3, 5):
+                continue
             if i == 5 and head:   # conv6 writes the classifier's chunk-major input
                 if "a6k" not in b:
                     b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)

@@ -115,6 +115,21 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
                               const int32_t* corr2, int y_zp, int relu2, const qcn_qdq_t* qdq2,
                               uint8_t* y, void* stream);
 
+/* Two convolutions of one SimpleConvNet block in one launch: conv A
+ * (cin -> cmid, no pool) then conv B (cmid -> cout, fused 2x2 max-pool).  A's
+ * output never leaves LDS; the results are those of two qcn_conv3x3_u8s8_nhwc
+ * calls (A's u8 output zero point zmid is B's input zero point, or qdqa->z2 in
+ * QDQ mode; qdqa / qdqb may be NULL).  y: u8 NHWC [nimg, hw/2, hw/2, cout], or chunk-major like
+ * qcn_conv3x3_u8s8_kmajor when kmajor != 0.  Supported: (hw 16, 64 -> 128 ->
+ * 128) and (hw 8, 128 -> 256 -> 256) — SimpleConvNet conv3+conv4 and
+ * conv5+conv6; QCN_ERR_UNSUPPORTED otherwise. */
+int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
+                          const int8_t* wa_packed, int cmid, const float* ua, const float* va,
+                          const float* multa, const int32_t* corra, int zmid, int relua,
+                          const qcn_qdq_t* qdqa, const int8_t* wb_packed, int cout, const float* ub,
+                          const float* vb, const float* multb, const int32_t* corrb, int y_zp,
+                          int relub, const qcn_qdq_t* qdqb, int kmajor, uint8_t* y, void* stream);
+
 /* A5/A6 as above, but y is written chunk-major for the classifier head:
  * y[f / 32][nimg][32] with f the NHWC flatten index of one image's output
  * (oh * ow * cout bytes).  Supported: the 8x8 layers with cout == 256

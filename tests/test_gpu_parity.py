@@ -353,3 +353,52 @@ def test_conv_kmajor_output(dev, pool):
     assert ops.conv3x3_kmajor(T(qx), *args, out)
     torch.cuda.synchronize()
     assert torch.equal(ops.from_kmajor(out), ref.view(n, -1))
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
+    """Same for the per-layer QDQ model (both qdq hand-offs inside a pair)."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load(per_channel)
+    spec = netfix.qdq_spec(z)
+    x = torch.from_numpy(netfix.images(z)).to(dev)
+    model = QuantizedConvNet(spec, dev)
+    assert "conv34" in model.kernel_names(x.shape)
+    out_p = model.run(x).clone()
+    a4_p = model._bufs[x.shape[0]]["a4"].clone()
+    model.fuse_pairs = False
+    out_l = model.run(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a4_p, model._bufs[x.shape[0]]["a4"])
+    assert torch.equal(out_p, out_l)
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_conv_pairs_equal_layerwise(dev, per_channel):
+    """conv3+conv4 and conv5+conv6 as fused block launches (middle activation
+    in LDS only) give the per-layer kernels' outputs bit for bit — the
+    conv4 output, the chunk-major conv6 output and the logits — and the
+    per-layer path itself matches the golden fixture (test_full_net_*)."""
+    import netfix
+    from qconvnet import ops
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load(per_channel)
+    spec, _ = netfix.static_spec(z)
+    x = torch.from_numpy(netfix.images(z)).to(dev)
+    n = x.shape[0]
+    model = QuantizedConvNet(spec, dev)
+    assert "conv34" in model.kernel_names(x.shape)
+    out_p = model.run(x).clone()
+    b = model._bufs[n]
+    a4_p = b["a4"].clone()
+    a6_p = (ops.from_kmajor(b["a6k"]).clone() if model._head_fused(n) else b["a6"].reshape(n, -1).clone())
+    model.fuse_pairs = False
+    out_l = model.run(x).clone()
+    b = model._bufs[n]
+    a6_l = (ops.from_kmajor(b["a6k"]) if model._head_fused(n) else b["a6"].reshape(n, -1))
+    torch.cuda.synchronize()
+    assert torch.equal(a4_p, b["a4"])
+    assert torch.equal(a6_p, a6_l)
+    assert torch.equal(out_p, out_l)
+    assert np.array_equal(out_p.cpu().numpy(), z["logits"])

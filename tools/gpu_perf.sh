@@ -1,14 +1,15 @@
-# GPU perf pass: parity gate, bench, kernel trace, PMC counters (separate passes).
+# GPU perf pass: parity gate, the default bench line (with CPU baselines), kernel
+# trace of the same command, PMC counters (separate passes, as the guide says).
 # usage (on the box, from the repo root): bash tools/gpu_perf.sh TAG
 set -e
 TAG=${1:-run}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > $O/parity.log 2>&1
-timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu > $O/bench.json 2> $O/bench.err
+timeout -k 10 300 python -m pytest tests -x -q -m gpu > $O/gpu_tests.log 2>&1
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu > $O/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- python3 $R/bench.py --no-cpu > $O/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU -f csv -d $O/pmc_sq -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu > $O/pmc_sq.log 2>&1 || echo "pmc_sq failed" >> $O/errors.txt
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu > $O/pmc_fetch.log 2>&1 || echo "pmc_fetch failed" >> $O/errors.txt
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu > $O/pmc_write.log 2>&1 || echo "pmc_write failed" >> $O/errors.txt
