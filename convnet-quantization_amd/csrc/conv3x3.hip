@@ -158,7 +158,7 @@ QCN_DEV void stage_epik(const ConvEpi& ep, float* ek, int tid) {
 // rounds half-to-even and saturates to [0, 255] (probed exhaustively on gfx950,
 // tools/micro/cvt_probe.hip), and the fma / mul run as packed fp32 pairs:
 // 3 VALU per element instead of 7 (the epilogue is VALU-issue bound).
-template <int NQ, bool XORIN, bool FAST>
+template <int NQ, bool XORIN, bool FAST, bool D32 = false>
 QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
                              int hi, uint8_t* orow) {
   // accumulators already include the zero-point correction (acc_init_corr)
@@ -197,6 +197,14 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
     }
     w[g] = wd;
   }
+  if constexpr (D32) {
+    // the lane's 4-channel groups 8g + 4hi straight to their dwords of the
+    // destination row (v_permlane32_swap costs ~25 cycles each)
+    uint32_t* od = reinterpret_cast<uint32_t*>(orow + co_base) + hi;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) od[2 * g] = XORIN ? xor80(w[g]) : w[g];
+    return;
+  }
   // low lanes: c0-3 | c8-11 | c16-19 | c24-27 ; high lanes: c4-7 | c12-15 | ...
   auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
   auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
@@ -214,11 +222,11 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
 
 QCN_DEV bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
 
-template <int NQ, bool XORIN = false>
+template <int NQ, bool XORIN = false, bool D32 = false>
 QCN_DEV void epilogue_tile_kf(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
                               int hi, uint8_t* orow) {
-  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true>(accs, K, ep, co_base, hi, orow);
-  else epilogue_tile_k<NQ, XORIN, false>(accs, K, ep, co_base, hi, orow);
+  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true, D32>(accs, K, ep, co_base, hi, orow);
+  else epilogue_tile_k<NQ, XORIN, false, D32>(accs, K, ep, co_base, hi, orow);
 }
 
 template <int NQ, bool XORIN = false>
@@ -433,7 +441,6 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
     }
   }
   __syncthreads();
-  QCN_STAMP(4);
   const long out0 = (long)blockIdx.x * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
   if (ep.kmajor) {
@@ -570,12 +577,15 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int y0 = (int)((p0 % CA::IMG) / CA::W);
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  QCN_STAMP(0);
   stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
   stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
+  QCN_STAMP(1);
 
   v16i acc[2][4];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
+  QCN_STAMP(2);
 
   // ---- A's epilogue into B's patch (A's patch and ring are dead past the
   // main loop's final barrier): zero-point halo, then the requantized interior
@@ -603,13 +613,21 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
       for (int j = 0; j < 4; ++j) {
         const int m = (wp * 4 + j) * 32 + l32;
         const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
+#ifdef QCN_EXP_PAIR_PERM
         epilogue_tile_kf<1, true>(&acc[i][j], K, epa, co_base, hi, lds + CB::slot(seg, row + 1, col + 1));
+#else
+        epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
+                                        lds + CB::slot(seg, row + 1, col + 1));
+#endif
       }
     }
   }
   __syncthreads();
+  QCN_STAMP(3);
   conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
+  QCN_STAMP(4);
   conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, ekb);
+  QCN_STAMP(5);
 }
 
 // --------------------------------------------------------------------------

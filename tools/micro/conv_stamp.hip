@@ -124,8 +124,36 @@ static void run12(int nimg) {
   });
 }
 
+static void runpair(int cin, int cmid, int cout, int hw, int nimg) {
+  const long nin = (long)nimg * hw * hw * cin;
+  std::vector<uint8_t> hx(nin);
+  for (auto& e : hx) e = (uint8_t)r8();
+  std::vector<int8_t> wa((long)cmid * cin * 9), wb((long)cout * cmid * 9), pa(wa.size()), pb(wb.size());
+  for (auto& e : wa) e = r8();
+  for (auto& e : wb) e = r8();
+  std::vector<int32_t> sa(cmid), sb(cout), ca(cmid), cb(cout);
+  qcn_pack_conv3x3_weight(wa.data(), cmid, cin, pa.data(), sa.data());
+  qcn_pack_conv3x3_weight(wb.data(), cout, cmid, pb.data(), sb.data());
+  for (int i = 0; i < cmid; ++i) ca[i] = (128 - 3) * sa[i];
+  for (int i = 0; i < cout; ++i) cb[i] = 128 * sb[i];
+  uint8_t* dx = up(hx); int8_t* dwa = up(pa); int8_t* dwb = up(pb); int* dca = up(ca); int* dcb = up(cb);
+  float* dua = up(std::vector<float>(cmid, 0.5f)); float* dva = up(std::vector<float>(cmid, 1.0f));
+  float* dma = up(std::vector<float>(cmid, 1e-3f));
+  float* dub = up(std::vector<float>(cout, 0.5f)); float* dvb = up(std::vector<float>(cout, 1.0f));
+  float* dmb = up(std::vector<float>(cout, 1e-3f));
+  uint8_t* dy; CK(hipMalloc(&dy, (long)nimg * hw * hw / 4 * cout));
+  char title[128];
+  snprintf(title, sizeof title, "pair %d->%d->%d @%d (pool) n=%d  [stage|A|A-epi|B|B-epi]", cin, cmid, cout, hw, nimg);
+  report(title, (double)nimg * hw * hw * (cmid * cin + cout * cmid) * 9, [&] {
+    qcn_conv3x3_pair_u8s8(dx, nimg, hw, cin, 3, dwa, cmid, dua, dva, dma, dca, 0, 1, nullptr, dwb, cout,
+                          dub, dvb, dmb, dcb, 0, 1, nullptr, 0, dy, 0);
+  });
+}
+
 int main() {
   const int n = 1024;
+  runpair(64, 128, 128, 16, n);
+  runpair(128, 256, 256, 8, n);
   run12(n);
   run(64, 128, 16, 0, n);   // conv3
   run(128, 128, 16, 1, n);  // conv4
