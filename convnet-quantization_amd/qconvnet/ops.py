@@ -287,3 +287,89 @@ def linear_f32(x, w, b, relu_in=False, out=None):
     check(lib().qcn_linear_f32(_ptr(x), m, k, _ptr(w), n, _ptr(b), int(bool(relu_in)), _ptr(out),
                                _stream()), "linear_f32")
     return out
+
+
+# ------------------------------------------------ ResNet blocks
+def pack_conv_kmajor(w_oihw: np.ndarray):
+    """s8 OIHW -> (chunk-major [kh*kw*cin/32, cout, 32] bytes, wsum int32)."""
+    w = np.ascontiguousarray(w_oihw, dtype=np.int8)
+    cout, cin, kh, kw = w.shape
+    out = np.empty((kh * kw * cin // 32, cout, 32), np.int8)
+    wsum = np.empty(cout, np.int32)
+    check(lib().qcn_pack_conv_weight_kmajor(w.ctypes.data, cout, cin, kh, kw, out.ctypes.data,
+                                            wsum.ctypes.data), "pack_conv_kmajor")
+    return out, wsum
+
+
+def stem_weight_rows(w_oihw: np.ndarray):
+    """7x7 stem weights [k][3][7][7] -> the 7x1 conv over the packed rows
+    (qcn_stem_pack_f32_nchw): [k][32][7][1], channel 3*s + c holds w[k][c][r][s]."""
+    w = np.asarray(w_oihw)
+    k, c, kh, kw = w.shape
+    if c * kw > 32:
+        raise ValueError("stem rows need c * kw <= 32")
+    out = np.zeros((k, 32, kh, 1), w.dtype)
+    out[:, :c * kw, :, 0] = np.transpose(w, (0, 3, 1, 2)).reshape(k, kw * c, kh)
+    return out
+
+
+def conv(x, x_zp, layer, out=None):
+    """Generic quantized conv on u8 NHWC.  ``layer`` carries w (packed), cout,
+    kh, kw, stride (sy, sx), pad (py, px), u, v, mult, corr, z_y, relu."""
+    _need(x, torch.uint8, "conv.x")
+    n, h, w, cin = x.shape
+    d = layer
+    oh = (h + 2 * d.py - d.kh) // d.sy + 1
+    ow = (w + 2 * d.px - d.kw) // d.sx + 1
+    if out is None:
+        out = torch.empty((n, oh, ow, d.cout), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_conv_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, d.kh, d.kw,
+                                   d.sy, d.sx, d.py, d.px, _ptr(d.u), _ptr(d.v), _ptr(d.mult),
+                                   _ptr(d.corr), int(d.z_y), int(bool(d.relu)), _ptr(out),
+                                   _stream()), "conv")
+    return out
+
+
+def add_relu(a, sa, za, b, sb, zb, s_out, z_out, relu=True, out=None):
+    _need(a, torch.uint8, "add.a")
+    _need(b, torch.uint8, "add.b")
+    if a.shape != b.shape:
+        raise ValueError("add_relu operands differ in shape")
+    if out is None:
+        out = torch.empty_like(a)
+    check(lib().qcn_add_relu_u8(_ptr(a), float(sa), int(za), _ptr(b), float(sb), int(zb), a.numel(),
+                                float(s_out), int(z_out), int(bool(relu)), _ptr(out), _stream()),
+          "add_relu")
+    return out
+
+
+def maxpool3x3s2(x, out=None):
+    _need(x, torch.uint8, "maxpool3.x")
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c), dtype=torch.uint8,
+                          device=x.device)
+    check(lib().qcn_maxpool3x3s2_u8_nhwc(_ptr(x), n, h, w, c, _ptr(out), _stream()), "maxpool3x3s2")
+    return out
+
+
+def stem_pack(x, scale, zp, out=None):
+    _need(x, torch.float32, "stem.x")
+    n, c, h, w = x.shape
+    if c != 3:
+        raise ValueError("stem_pack expects 3 input channels")
+    if out is None:
+        out = torch.empty((n, h, (w - 1) // 2 + 1, 32), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_stem_pack_f32_nchw(_ptr(x), n, h, w, float(scale), int(zp), _ptr(out),
+                                       _stream()), "stem_pack")
+    return out
+
+
+def avgpool(x, x_scale, x_zp, s_out, z_out, out=None):
+    _need(x, torch.uint8, "avgpool.x")
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, c), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_avgpool_u8_nhwc(_ptr(x), n, h * w, c, float(x_scale), int(x_zp), float(s_out),
+                                    int(z_out), _ptr(out), _stream()), "avgpool")
+    return out

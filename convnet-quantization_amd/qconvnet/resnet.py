@@ -1,0 +1,318 @@
+"""Static int8 ResNet (bottleneck blocks, per-channel weights) on MI355X —
+SURVEY §8(f)2, BASELINE config 5.
+
+Reference: ``CustomQuantizedBottleneck`` / ``CustomQuantizedResNet50``
+(models/custom_quantization_model.py:60-148) around torchvision's ResNet-50
+(models/dynamic_ptq_model.py:194-195).  Semantics, as for the SimpleConvNet
+static path (qmodel.py): BN folded into each conv (custom_quantization_model.py
+:264-291 fuses the same Conv-BN(-ReLU) triples), ReLU fused into the requant,
+per-channel symmetric s8 weights, u8 per-tensor affine activations with
+MinMax ranges observed on calibration data.  The residual join keeps the
+reference's float-domain add (:94-101): both operands are dequantized, added
+in fp32, ReLU'd and quantized with the block output's qparams.
+
+Device pipeline per forward (all u8 NHWC, every launch a hand-written HIP
+kernel on the current stream, capturable into a HIP graph):
+  stem_pack (QuantStub + 7-tap row im2col) -> conv 7x1 (the 7x7/2 stem) ->
+  maxpool 3x3/2 -> 16 x [conv1x1+ReLU -> conv3x3(/2)+ReLU -> conv1x1
+  (-> downsample conv1x1(/2)) -> add+ReLU] -> avgpool+quantize -> fc (fp32 logits)
+"""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from . import quant as Q
+from .qmodel import _DevLayer, _Range, _weight_scale
+
+F32 = np.float32
+
+
+# ============================================================ fp32 folding
+def _np(v):
+    return v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+
+
+def _fold(g, conv, bn):
+    return Q.fold_bn(g[conv + ".weight"], g.get(conv + ".bias"), g[bn + ".running_mean"],
+                     g[bn + ".running_var"], g[bn + ".weight"], g[bn + ".bias"])
+
+
+def fold_state_dict(sd):
+    """BN-fold a torchvision-layout ResNet state_dict.  Returns
+    {"stem": (w, b), "blocks": [{"c1","c2","c3"[, "ds"]: (w, b, stride, pad)}],
+     "fc": (w, b)}; strides follow torchvision (first block of layer2..4
+    strides its 3x3 conv and its downsample)."""
+    g = {k: _np(v) for k, v in sd.items()}
+    out = {"stem": _fold(g, "conv1", "bn1"), "blocks": []}
+    keys = sorted({(int(m.group(1)), int(m.group(2)))
+                   for k in g for m in [re.match(r"layer(\d)\.(\d+)\.conv1\.weight$", k)] if m})
+    for li, bi in keys:
+        p = f"layer{li}.{bi}."
+        s = 2 if (bi == 0 and li > 1) else 1
+        blk = {}
+        for j, (st, pad) in enumerate(((1, 0), (s, 1), (1, 0)), start=1):
+            w, b = _fold(g, p + f"conv{j}", p + f"bn{j}")
+            blk[f"c{j}"] = (w, b, st, pad)
+        if p + "downsample.0.weight" in g:
+            w, b = _fold(g, p + "downsample.0", p + "downsample.1")
+            blk["ds"] = (w, b, s, 0)
+        out["blocks"].append(blk)
+    out["fc"] = (np.asarray(g["fc.weight"], F32), np.asarray(g["fc.bias"], F32))
+    return out
+
+
+# ============================================================ calibration
+def calibrate(folded, batches, device="cuda"):
+    """fp32 forward of the folded net recording every observer's range:
+    x, stem (post-ReLU), per block c1/c2 (post-ReLU), c3 and ds (pre-add),
+    out (post add+ReLU), pool (avgpool output), fc."""
+    dev = torch.device(device)
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    stem = [t(a) for a in folded["stem"]]
+    blocks = [{k: (t(v[0]), t(v[1]), v[2], v[3]) for k, v in b.items()} for b in folded["blocks"]]
+    fc = [t(a) for a in folded["fc"]]
+    rng = {"x": _Range(dev), "stem": _Range(dev), "pool": _Range(dev), "fc": _Range(dev)}
+    for i, b in enumerate(blocks):
+        for k in list(b) + ["out"]:
+            rng[f"b{i}.{k}"] = _Range(dev)
+    with torch.no_grad():
+        for xb in batches:
+            x = xb.to(dev, torch.float32)
+            rng["x"](x)
+            x = F.relu(F.conv2d(x, stem[0], stem[1], stride=2, padding=3))
+            rng["stem"](x)
+            x = F.max_pool2d(x, 3, 2, 1)
+            for i, b in enumerate(blocks):
+                def cv(inp, k):
+                    w, bb, s, p = b[k]
+                    return F.conv2d(inp, w, bb, stride=s, padding=p)
+                y = F.relu(cv(x, "c1"))
+                rng[f"b{i}.c1"](y)
+                y = F.relu(cv(y, "c2"))
+                rng[f"b{i}.c2"](y)
+                y = cv(y, "c3")
+                rng[f"b{i}.c3"](y)
+                idn = x
+                if "ds" in b:
+                    idn = cv(x, "ds")
+                    rng[f"b{i}.ds"](idn)
+                x = F.relu(y + idn)
+                rng[f"b{i}.out"](x)
+            x = x.mean((2, 3))
+            rng["pool"](x)
+            x = F.linear(x, fc[0], fc[1])
+            rng["fc"](x)
+    return {k: r.values() for k, r in rng.items()}
+
+
+# ============================================================ quantized spec
+def build_spec(folded, ranges, per_channel=True):
+    """Host description of the int8 net (numpy), the format
+    oracle.qref.resnet_int8_forward reads."""
+    def layer(wb, s_x, z_x, name, relu):
+        w, b, st, pad = wb
+        s_w = _weight_scale(w, per_channel)
+        s_y, z_y = Q.qparams_affine(*ranges[name])
+        return dict(w=Q.quantize_weight(w, s_w), b=np.asarray(b, F32), s_w=s_w, s_x=s_x, z_x=z_x,
+                    s_y=s_y, z_y=z_y, relu=relu, stride=(st, st), pad=(pad, pad))
+
+    spec = {"per_channel": bool(per_channel), "blocks": []}
+    s_x, z_x = Q.qparams_affine(*ranges["x"])
+    spec["in"] = (s_x, z_x)
+    w, b = folded["stem"]
+    spec["stem"] = layer((w, b, 2, 3), s_x, z_x, "stem", True)
+    s_x, z_x = spec["stem"]["s_y"], spec["stem"]["z_y"]
+    for i, blk in enumerate(folded["blocks"]):
+        e = {"c1": layer(blk["c1"], s_x, z_x, f"b{i}.c1", True)}
+        e["c2"] = layer(blk["c2"], e["c1"]["s_y"], e["c1"]["z_y"], f"b{i}.c2", True)
+        e["c3"] = layer(blk["c3"], e["c2"]["s_y"], e["c2"]["z_y"], f"b{i}.c3", False)
+        e["ds"] = layer(blk["ds"], s_x, z_x, f"b{i}.ds", False) if "ds" in blk else None
+        e["out"] = Q.qparams_affine(*ranges[f"b{i}.out"])
+        spec["blocks"].append(e)
+        s_x, z_x = e["out"]
+    spec["pool"] = Q.qparams_affine(*ranges["pool"])
+    w, b = folded["fc"]
+    s_w = _weight_scale(w, per_channel)
+    s_y, z_y = Q.qparams_affine(*ranges["fc"])
+    spec["fc"] = dict(w=Q.quantize_weight(w, s_w), b=np.asarray(b, F32), s_w=s_w,
+                      s_x=spec["pool"][0], z_x=spec["pool"][1], s_y=s_y, z_y=z_y, relu=False)
+    return spec
+
+
+def quantize_resnet(model, calib_batches, device="cuda", per_channel=True):
+    """fp32 ResNet (models.resnet / torchvision layout) -> QuantizedResNet."""
+    folded = fold_state_dict(model.state_dict())
+    ranges = calibrate(folded, calib_batches, device)
+    return QuantizedResNet(build_spec(folded, ranges, per_channel), device)
+
+
+# ============================================================ device model
+class QuantizedResNet:
+    """Duck-typed int8 ResNet (eval / cpu / to / __call__ like the reference's
+    models.*): fp32 [N,3,H,W] in, fp32 [N,num_classes] logits out."""
+
+    def __init__(self, spec, device="cuda"):
+        self.spec = spec
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the int8 path runs on the GPU (HIP); pass a cuda device")
+        self.quantized = True
+        self.host_io = False
+        self._graphs = {}
+        self._upload()
+
+    def _t(self, a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+
+    def _layer(self, e, stem=False):
+        d = _DevLayer()
+        w = np.asarray(e["w"], np.int8)
+        if stem:
+            w = ops.stem_weight_rows(w)
+            d.sy, d.sx, d.py, d.px = e["stride"][0], 1, e["pad"][0], 0
+        else:
+            (d.sy, d.sx), (d.py, d.px) = e["stride"], e["pad"]
+        packed, wsum = ops.pack_conv_kmajor(w)
+        d.cout, _, d.kh, d.kw = w.shape
+        u, v, mult = Q.epilogue_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
+        d.w = self._t(packed)
+        d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
+        d.corr = self._t(((128 - int(e["z_x"])) * wsum.astype(np.int64)).astype(np.int32))
+        d.z_x, d.z_y, d.s_y, d.relu = int(e["z_x"]), int(e["z_y"]), F32(e["s_y"]), e["relu"]
+        return d
+
+    def _upload(self):
+        sp = self.spec
+        self.in_scale, self.in_zp = sp["in"]
+        self.stem = self._layer(sp["stem"], stem=True)
+        self.blocks = []
+        for e in sp["blocks"]:
+            self.blocks.append({k: (self._layer(e[k]) if e.get(k) is not None else None)
+                                for k in ("c1", "c2", "c3", "ds")})
+        fc = sp["fc"]
+        d = _DevLayer()
+        w = np.asarray(fc["w"], np.int8)
+        u, v, mult = Q.epilogue_constants(fc["s_x"], fc["s_w"], fc["s_y"], fc["b"])
+        d.w = self._t(w)
+        d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
+        d.corr = self._t(((128 - int(fc["z_x"])) * w.astype(np.int64).sum(1)).astype(np.int32))
+        d.z_x, d.z_y, d.s_y = int(fc["z_x"]), int(fc["z_y"]), F32(fc["s_y"])
+        self.fc = d
+        self.num_classes = w.shape[0]
+
+    def conv_layers(self):
+        """Every conv launch in forward order (for MAC accounting)."""
+        out = [self.stem]
+        for b in self.blocks:
+            out += [b["c1"], b["c2"], b["c3"]] + ([b["ds"]] if b["ds"] is not None else [])
+        return out
+
+    def run(self, x, keep=False, marks=None):
+        """The whole int8 forward on the current stream (no sync)."""
+        inter = {}
+
+        def mark(name):
+            if marks is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                marks.append((name, ev))
+
+        sp = self.spec
+        mark("start")
+        q = ops.stem_pack(x, self.in_scale, self.in_zp)
+        mark("stem_pack")
+        q = ops.conv(q, self.in_zp, self.stem)
+        mark("conv")
+        q = ops.maxpool3x3s2(q)
+        mark("maxpool")
+        if keep:
+            inter["stem"] = q
+        for i, (b, e) in enumerate(zip(self.blocks, sp["blocks"])):
+            zx = b["c1"].z_x
+            y = ops.conv(q, zx, b["c1"])
+            mark("conv")
+            y = ops.conv(y, b["c2"].z_x, b["c2"])
+            mark("conv")
+            y = ops.conv(y, b["c3"].z_x, b["c3"])
+            mark("conv")
+            if b["ds"] is not None:
+                idn = ops.conv(q, zx, b["ds"])
+                mark("conv")
+                si, zi = e["ds"]["s_y"], e["ds"]["z_y"]
+            else:
+                idn, si, zi = q, e["c1"]["s_x"], zx
+            so, zo = e["out"]
+            q = ops.add_relu(y, e["c3"]["s_y"], e["c3"]["z_y"], idn, si, zi, so, zo, True)
+            mark("add")
+            if keep:
+                inter[f"block{i}"] = q
+        last = sp["blocks"][-1]["out"] if sp["blocks"] else (sp["stem"]["s_y"], sp["stem"]["z_y"])
+        sp_, zp_ = sp["pool"]
+        q = ops.avgpool(q, last[0], last[1], sp_, zp_)
+        mark("avgpool")
+        if keep:
+            inter["pool"] = q
+        f = self.fc
+        qy, logits = ops.linear_u8(q, f.z_x, f.w, f.u, f.v, f.mult, f.corr, f.z_y, False,
+                                   y_scale=f.s_y, want_fp32=True)
+        mark("fc")
+        return (logits, inter) if keep else logits
+
+    def capture_graph(self, x_static):
+        n = x_static.shape[0]
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.run(x_static)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self.run(x_static)
+        self._graphs[n] = (g, x_static, out)
+        return g
+
+    def replay(self, n):
+        g, _, out = self._graphs[n]
+        g.replay()
+        return out
+
+    @torch.no_grad()
+    def forward(self, x):
+        host = not x.is_cuda
+        xd = x.to(self.device, torch.float32).contiguous()
+        out = self.run(xd).clone()
+        if host or self.host_io:
+            return out.cpu()
+        torch.cuda.current_stream(self.device).synchronize()
+        return out
+
+    __call__ = forward
+
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise RuntimeError("QuantizedResNet is inference-only")
+        return self
+
+    def to(self, device):
+        if torch.device(device).type == "cpu":
+            self.host_io = True
+        return self
+
+    def cpu(self):
+        self.host_io = True
+        return self
+
+    def cuda(self, device=None):
+        self.host_io = False
+        return self

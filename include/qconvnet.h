@@ -186,6 +186,42 @@ int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
 int qcn_linear_f32(const float* x, int m, int k, const float* w, int n, const float* b,
                    int relu_in, float* y, void* stream);
 
+/* ---- ResNet-style bottleneck blocks (config 5) ----------
+ * CustomQuantizedBottleneck / CustomQuantizedResNet50
+ * (models/custom_quantization_model.py:60-148): 1x1, 3x3 (strided) and 1x1
+ * downsample convs, the fp32-domain residual add + ReLU (:94-101), the stem
+ * conv + maxpool, the global average pool and the fc classifier. */
+
+/* Host: s8 OIHW [cout][cin][kh][kw] -> chunk-major [kh*kw*cin/32][cout][32]
+ * (K ordered (r, s, c)); wsum[cout] = sum of each filter.  cin % 32 == 0. */
+int qcn_pack_conv_weight_kmajor(const int8_t* w_oihw, int cout, int cin, int kh, int kw,
+                                int8_t* out, int32_t* wsum);
+/* Quantized Conv2d(+ReLU) (QuantizedConv2d / QuantizedConvReLU2d with
+ * per-channel or per-tensor weights) on u8 NHWC, any kernel / stride /
+ * padding; requant as qcn_conv3x3_u8s8_nhwc (A6).  cin % 32 == 0,
+ * cout % 64 == 0; corr = (128 - x_zp) * wsum.  Output [n][oh][ow][cout]. */
+int qcn_conv_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                       const int8_t* w_packed, int cout, int kh, int kw, int stride_h,
+                       int stride_w, int pad_h, int pad_w, const float* u, const float* v,
+                       const float* mult, const int32_t* corr, int y_zp, int relu, uint8_t* y,
+                       void* stream);
+/* Residual join (custom_quantization_model.py:94-101 then the next stage's
+ * QuantStub): y = quantize(relu?(fp32(sa*(a-za)) + fp32(sb*(b-zb))), s_out, z_out). */
+int qcn_add_relu_u8(const uint8_t* a, float sa, int za, const uint8_t* b, float sb, int zb,
+                    long long count, float s_out, int z_out, int relu, uint8_t* y, void* stream);
+/* nn.MaxPool2d(3, 2, padding=1) on u8 NHWC (c % 16 == 0). */
+int qcn_maxpool3x3s2_u8_nhwc(const uint8_t* x, int nimg, int h, int w, int c, uint8_t* y,
+                             void* stream);
+/* QuantStub on fp32 NCHW [n][3][h][w] fused with the row im2col of the 7x7 /
+ * stride-2 / pad-3 stem: y[n][h][ow][32], byte 3*s+ch = q(x[n][ch][iy][2*ox-3+s]),
+ * zero point outside the image and in bytes 21..31.  ow = (w-1)/2 + 1. */
+int qcn_stem_pack_f32_nchw(const float* x, int nimg, int h, int w, float scale, int zp, uint8_t* y,
+                           void* stream);
+/* AdaptiveAvgPool2d(1) + the fc's QuantStub: y[n][c] =
+ * quantize(fp32(sum_q - hw*x_zp) * fp32(x_scale/hw), s_out, z_out). */
+int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, float x_scale, int x_zp,
+                        float s_out, int z_out, uint8_t* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -303,9 +303,82 @@ def gen_net(per_channel=False, batch=64):
     return rec
 
 
+# ------------------------------------------- SURVEY §8(f)2 (ResNet blocks)
+def _convgen_case(rng, n, h, cin, cout, k, stride, pad, zx, relu, per_channel, zy):
+    s_x = F32(rng.uniform(0.01, 0.03))
+    qx = rng.integers(0, 256, (n, h, h, cin)).astype(np.uint8)
+    w = (rng.standard_normal((cout, cin, k, k)) * 0.05).astype(F32)
+    b = (rng.standard_normal(cout) * 0.5).astype(F32)
+    if per_channel:
+        s_w, _ = qref.qparams_symmetric(w.reshape(cout, -1).min(1), w.reshape(cout, -1).max(1))
+        wq = torch.quantize_per_channel(torch.from_numpy(w), torch.from_numpy(s_w.astype(np.float64)),
+                                        torch.zeros(cout, dtype=torch.long), 0, torch.qint8)
+    else:
+        s_w, _ = qref.qparams_symmetric(w.min(), w.max())
+        wq = torch.quantize_per_tensor(torch.from_numpy(w), float(s_w), 0, torch.qint8)
+    wi = wq.int_repr().numpy()
+    assert (qref.quantize_weight(w, s_w) == wi).all()
+    s_y = F32(rng.uniform(0.01, 0.05))
+    mod = (nniq.ConvReLU2d if relu else nnq.Conv2d)(cin, cout, k, stride=stride, padding=pad)
+    mod.set_weight_bias(wq, torch.from_numpy(b))
+    mod.scale, mod.zero_point = float(s_y), int(zy)
+    xin = torch._make_per_tensor_quantized_tensor(
+        torch.from_numpy(np.ascontiguousarray(qx.transpose(0, 3, 1, 2))), float(s_x), int(zx))
+    out = mod(xin).int_repr().permute(0, 2, 3, 1).contiguous().numpy()
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    mine = qref.conv_q(qx, zx, wi, u, v, mult, zy, relu, (stride, stride), (pad, pad))
+    assert (mine == out).all(), f"general conv case mismatch {(mine != out).sum()}"
+    return dict(qx=qx, zx=np.int64(zx), s_x=s_x, w=wi, s_w=np.asarray(s_w, F32), b=b, s_y=s_y,
+                zy=np.int64(zy), relu=np.int64(relu), stride=np.int64(stride), pad=np.int64(pad),
+                out=out)
+
+
+def gen_resnet_ops(rng):
+    """General convs (1x1, strided 3x3, strided 1x1 downsample, the 7x7/2 stem)
+    against torch.ao's QuantizedConv(ReLU)2d; the residual join against aten
+    dequantize + add + relu + quantize_per_tensor; maxpool 3x3/2 against
+    torch's quantized max_pool2d."""
+    cases = {}
+    specs = [  # n, h, cin, cout, k, stride, pad, zx, relu, per_channel, zy
+        (2, 8, 64, 64, 1, 1, 0, 0, True, True, 0),
+        (2, 8, 64, 256, 1, 1, 0, 0, False, True, 121),
+        (2, 9, 64, 64, 3, 2, 1, 3, True, True, 0),
+        (2, 8, 128, 256, 1, 2, 0, 0, False, True, 64),
+        (2, 8, 32, 128, 3, 1, 1, 200, True, False, 0),
+        (1, 17, 3, 64, 7, 2, 3, 114, True, True, 0),
+    ]
+    for i, sp in enumerate(specs):
+        for k, v in _convgen_case(rng, *sp).items():
+            cases[f"c{i}_{k}"] = v
+    cases["n"] = np.int64(len(specs))
+    # residual join: out.dequantize() + identity.dequantize(), relu, quantize
+    adds = [(0.021, 130, 0.017, 0, 0.03, 0), (0.05, 0, 0.05, 0, 0.061, 0), (0.013, 255, 0.02, 7, 0.01, 0)]
+    for i, (sa, za, sb, zb, so, zo) in enumerate(adds):
+        qa = rng.integers(0, 256, (2, 7, 7, 64)).astype(np.uint8)
+        qb = rng.integers(0, 256, (2, 7, 7, 64)).astype(np.uint8)
+        ta = torch._make_per_tensor_quantized_tensor(torch.from_numpy(qa), sa, za)
+        tb = torch._make_per_tensor_quantized_tensor(torch.from_numpy(qb), sb, zb)
+        s = torch.relu(ta.dequantize() + tb.dequantize())
+        out = torch.quantize_per_tensor(s, so, zo, torch.quint8).int_repr().numpy()
+        mine = qref.add_relu_q(qa, sa, za, qb, sb, zb, so, zo, True)
+        assert (mine == out).all(), "add case mismatch"
+        cases.update({f"a{i}_qa": qa, f"a{i}_qb": qb, f"a{i}_p": np.array([sa, sb, so], F32),
+                      f"a{i}_z": np.array([za, zb, zo], np.int64), f"a{i}_out": out})
+    cases["na"] = np.int64(len(adds))
+    qm = rng.integers(0, 256, (2, 15, 15, 64)).astype(np.uint8)
+    tq = torch._make_per_tensor_quantized_tensor(torch.from_numpy(qm.transpose(0, 3, 1, 2).copy()), 0.1, 3)
+    mp = torch.nn.functional.max_pool2d(tq, 3, 2, 1).int_repr().permute(0, 2, 3, 1).contiguous().numpy()
+    assert (qref.maxpool3x3s2_nhwc(qm) == mp).all()
+    cases["mp_in"], cases["mp_out"] = qm, mp
+    np.savez_compressed(os.path.join(OUT, "ops_resnet.npz"), **cases)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.backends.quantized.engine = "fbgemm"
+    if sys.argv[1:] == ["resnet"]:   # only the §8(f)2 vectors
+        gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
+        return
     rng = np.random.Generator(np.random.PCG64(1234))
     gen_quantize(rng)
     gen_qparams(rng)
@@ -314,6 +387,7 @@ def main():
     gen_dynamic_linear(rng)
     gen_net(per_channel=False)
     gen_net(per_channel=True)
+    gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

@@ -348,3 +348,132 @@ def static_int8_forward(x_nchw, qm, keep=False):
                  qm["fc2_zp"], False)
     logits = dequantize(q, qm["fc2_scale"], qm["fc2_zp"])
     return logits, q, inter
+
+
+# ------------------------------------------- ResNet-style blocks
+# Reference: models/custom_quantization_model.py:60-148 (CustomQuantizedBottleneck,
+# CustomQuantizedResNet50) with torchvision's ResNet-50 topology (stem 7x7/2 conv,
+# 3x3/2 maxpool, [3,4,6,3] bottlenecks with the stride on the 3x3 conv and a
+# 1x1 strided downsample, global average pool, fc).  Static int8 semantics as in
+# static_int8_forward: BN folded into each conv, ReLU fused into the requant,
+# every activation u8 per-tensor affine; the residual join dequantizes both
+# operands and adds in fp32 (custom_quantization_model.py:94-101) before the
+# ReLU and the next stage's QuantStub.
+def conv_acc_nhwc(qx, zx, qw, stride=(1, 1), pad=(0, 0)):
+    """Exact int32 accumulator of a general conv (FBGEMM im2col pads with
+    q = z_x): acc[n,oy,ox,k] = sum_{r,s,c} (q_x - z_x) * q_w[k,c,r,s].
+    qx: [N,H,W,C] u8; qw: OIHW s8 (symmetric weights, zp 0).  The products are
+    summed in float64 — exact, since |sum| < 2^53 for any K below 2^37."""
+    n, h, w, c = qx.shape
+    k, c2, kh, kw = qw.shape
+    assert c2 == c, (c2, c)
+    sy, sx = stride
+    py, px = pad
+    oh, ow = (h + 2 * py - kh) // sy + 1, (w + 2 * px - kw) // sx + 1
+    xp = np.zeros((n, h + 2 * py, w + 2 * px, c), np.float64)
+    xp[:, py:py + h, px:px + w, :] = qx.astype(np.float64) - float(zx)
+    wt = qw.astype(np.float64)
+    acc = np.zeros((n * oh * ow, k), np.float64)
+    for r in range(kh):
+        for s in range(kw):
+            patch = xp[:, r:r + sy * (oh - 1) + 1:sy, s:s + sx * (ow - 1) + 1:sx, :]
+            acc += patch.reshape(-1, c) @ wt[:, :, r, s].T
+    return acc.reshape(n, oh, ow, k).astype(np.int64).astype(np.int32)
+
+
+def conv_q(qx, zx, qw, u, v, mult, zp_y, relu, stride=(1, 1), pad=(0, 0)):
+    """QuantizedConv2d / QuantizedConvReLU2d, any kernel/stride/padding."""
+    return requantize(conv_acc_nhwc(qx, zx, qw, stride, pad), u, v, mult, zp_y, relu)
+
+
+def add_relu_q(qa, sa, za, qb, sb, zb, s_out, z_out, relu=True):
+    """Residual join: out.dequantize() + identity.dequantize() in fp32, ReLU,
+    then quantize_per_tensor with the next stage's qparams
+    (custom_quantization_model.py:94-101)."""
+    s = (dequantize(qa, sa, za) + dequantize(qb, sb, zb)).astype(F32)
+    if relu:
+        s = np.maximum(s, F32(0.0))
+    return quantize_per_tensor(s, s_out, z_out)
+
+
+def maxpool3x3s2_nhwc(q):
+    """nn.MaxPool2d(3, 2, padding=1) (the ResNet stem); padding never wins."""
+    n, h, w, c = q.shape
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    xp = np.zeros((n, h + 2, w + 2, c), q.dtype)
+    xp[:, 1:h + 1, 1:w + 1, :] = q
+    out = np.zeros((n, oh, ow, c), q.dtype)
+    for r in range(3):
+        for s in range(3):
+            out = np.maximum(out, xp[:, r:r + 2 * (oh - 1) + 1:2, s:s + 2 * (ow - 1) + 1:2, :])
+    return out
+
+
+def avgpool_q(q, s_x, z_x, s_out, z_out):
+    """AdaptiveAvgPool2d(1) of the dequantized map, then the fc's QuantStub:
+    mean = fp32(sum_q - HW*z_x) * fp32(s_x / HW) (exact integer sum, two fp32
+    roundings — the definition qcn_avgpool_u8_nhwc implements)."""
+    n, h, w, c = q.shape
+    hw = h * w
+    tot = q.reshape(n, hw, c).astype(np.int64).sum(1) - hw * int(z_x)
+    k = F32(F32(s_x) / F32(hw))
+    mean = (tot.astype(F32) * k).astype(F32)
+    return quantize_per_tensor(mean, s_out, z_out)
+
+
+def stem_pack(x_nchw, scale, zp):
+    """Definition of qcn_stem_pack_f32_nchw (QuantStub + the row im2col of the
+    7x7/2/3 stem): [N,H,OW,32] with byte 3*s+c = q(x[n,c,iy,2*ox-3+s])."""
+    q = quantize_per_tensor(nchw_to_nhwc(np.asarray(x_nchw, F32)), scale, zp)
+    n, h, w, c = q.shape
+    ow = (w - 1) // 2 + 1
+    xp = np.full((n, h, w + 6, c), zp, np.uint8)
+    xp[:, :, 3:3 + w, :] = q
+    out = np.full((n, h, ow, 32), zp, np.uint8)
+    for s in range(7):
+        out[:, :, :, 3 * s:3 * s + c] = xp[:, :, s:s + 2 * (ow - 1) + 1:2, :]
+    return out
+
+
+def _layer_q(q, zx, e, relu):
+    u, v, mult = requant_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
+    return conv_q(q, zx, e["w"], u, v, mult, e["z_y"], relu, tuple(e["stride"]), tuple(e["pad"]))
+
+
+def bottleneck_int8_forward(q, blk):
+    """One bottleneck block on u8 NHWC (zero point blk['c1']['z_x'])."""
+    zx = blk["c1"]["z_x"]
+    y = _layer_q(q, zx, blk["c1"], True)
+    y = _layer_q(y, blk["c2"]["z_x"], blk["c2"], True)
+    y = _layer_q(y, blk["c3"]["z_x"], blk["c3"], False)
+    if blk.get("ds") is not None:
+        idn = _layer_q(q, zx, blk["ds"], False)
+        si, zi = blk["ds"]["s_y"], blk["ds"]["z_y"]
+    else:
+        idn, si, zi = q, blk["c1"]["s_x"], zx
+    so, zo = blk["out"]
+    return add_relu_q(y, blk["c3"]["s_y"], blk["c3"]["z_y"], idn, si, zi, so, zo, True)
+
+
+def resnet_int8_forward(x_nchw, spec, keep=False):
+    """Static-int8 ResNet forward (stem, maxpool, bottlenecks, avgpool, fc).
+    ``spec``: see qconvnet.resnet.build_spec.  Returns (logits fp32, inter)."""
+    inter = {}
+    s_in, z_in = spec["in"]
+    q = quantize_per_tensor(nchw_to_nhwc(np.asarray(x_nchw, F32)), s_in, z_in)
+    q = _layer_q(q, z_in, spec["stem"], True)
+    q = maxpool3x3s2_nhwc(q)
+    if keep:
+        inter["stem"] = q
+    for i, blk in enumerate(spec["blocks"]):
+        q = bottleneck_int8_forward(q, blk)
+        if keep:
+            inter[f"block{i}"] = q
+    last = spec["blocks"][-1]["out"] if spec["blocks"] else (spec["stem"]["s_y"], spec["stem"]["z_y"])
+    sp, zp = spec["pool"]
+    q = avgpool_q(q, last[0], last[1], sp, zp)
+    inter["pool"] = q
+    fc = spec["fc"]
+    u, v, mult = requant_constants(fc["s_x"], fc["s_w"], fc["s_y"], fc["b"])
+    qy = linear_q(q, fc["z_x"], fc["w"], u, v, mult, fc["z_y"], False)
+    return dequantize(qy, fc["s_y"], fc["z_y"]), inter

@@ -1,0 +1,170 @@
+"""GPU parity for SURVEY §8(f)2 (ResNet-style bottleneck blocks, config 5):
+the general int8 conv, residual join, maxpool 3x3/2, stem packing and average
+pool kernels (through the C ABI) against the torch.ao golden vectors and the
+numpy oracle, then whole networks (a 1-block-per-stage ResNet at 64x64 and the
+full ResNet-50 at 224x224) bit-exact against oracle.qref.resnet_int8_forward."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import qref
+
+pytestmark = pytest.mark.gpu
+
+F32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from qconvnet import _lib
+    _lib.load()
+    return torch.device("cuda:0")
+
+
+def _layer(dev, w_oihw, s_x, s_w, s_y, b, z_x, z_y, relu, stride, pad):
+    from qconvnet import ops
+    from qconvnet import quant as Q
+    from qconvnet.qmodel import _DevLayer
+    d = _DevLayer()
+    packed, wsum = ops.pack_conv_kmajor(w_oihw)
+    d.cout, _, d.kh, d.kw = w_oihw.shape
+    (d.sy, d.sx), (d.py, d.px) = stride, pad
+    u, v, mult = Q.epilogue_constants(s_x, s_w, s_y, b)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d.w, d.u, d.v, d.mult = t(packed), t(u), t(v), t(mult)
+    d.corr = t(((128 - int(z_x)) * wsum.astype(np.int64)).astype(np.int32))
+    d.z_y, d.relu = int(z_y), relu
+    return d
+
+
+def test_conv_general_golden(dev, golden_dir):
+    from qconvnet import ops
+    z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
+    ran = 0
+    for i in range(int(z["n"])):
+        g = lambda k: z[f"c{i}_{k}"]  # noqa: E731
+        if g("qx").shape[-1] % 32:
+            continue   # the 3-channel stem case runs through stem_pack (below)
+        st, pd = int(g("stride")), int(g("pad"))
+        d = _layer(dev, g("w"), g("s_x"), g("s_w"), g("s_y"), g("b"), int(g("zx")), int(g("zy")),
+                   bool(g("relu")), (st, st), (pd, pd))
+        out = ops.conv(torch.from_numpy(g("qx")).to(dev), int(g("zx")), d)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), g("out")), i
+        ran += 1
+    assert ran == 5
+
+
+@pytest.mark.parametrize("shape", [
+    # n, h, w, cin, cout, kh, kw, stride, pad, zx, relu, zy, per_channel
+    (3, 13, 11, 96, 192, 3, 3, 2, 1, 77, False, 30, True),
+    (1, 7, 7, 512, 2048, 1, 1, 1, 0, 0, False, 99, True),
+    (2, 14, 14, 256, 512, 1, 1, 2, 0, 4, False, 128, True),
+    (5, 9, 6, 32, 64, 3, 3, 1, 1, 255, True, 0, False),
+    (1, 1, 1, 64, 128, 3, 3, 1, 1, 13, True, 0, True),
+])
+def test_conv_general_oracle(dev, shape):
+    from qconvnet import ops
+    n, h, w, cin, cout, kh, kw, st, pd, zx, relu, zy, pc = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, h, w, cin)).astype(np.uint8)
+    wf = (rng.standard_normal((cout, cin, kh, kw)) * 0.05).astype(F32)
+    s_w = qref.qparams_symmetric(wf.reshape(cout, -1).min(1), wf.reshape(cout, -1).max(1))[0] if pc \
+        else qref.qparams_symmetric(wf.min(), wf.max())[0]
+    wq = qref.quantize_weight(wf, s_w)
+    b = (rng.standard_normal(cout) * 0.3).astype(F32)
+    s_x, s_y = F32(0.02), F32(0.9 if cin >= 256 else 0.2)
+    d = _layer(dev, wq, s_x, s_w, s_y, b, zx, zy, relu, (st, st), (pd, pd))
+    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d).cpu().numpy()
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, relu, (st, st), (pd, pd))
+    assert out.shape == ref.shape
+    assert np.array_equal(out, ref)
+    assert len(np.unique(ref)) > 8, "degenerate case"
+
+
+def test_add_relu_golden_and_ragged(dev, golden_dir):
+    from qconvnet import ops
+    z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
+    for i in range(int(z["na"])):
+        sa, sb, so = z[f"a{i}_p"]
+        za, zb, zo = (int(t) for t in z[f"a{i}_z"])
+        out = ops.add_relu(torch.from_numpy(z[f"a{i}_qa"]).to(dev), sa, za,
+                           torch.from_numpy(z[f"a{i}_qb"]).to(dev), sb, zb, so, zo)
+        assert np.array_equal(out.cpu().numpy(), z[f"a{i}_out"]), i
+    rng = np.random.default_rng(3)
+    for count in (1, 15, 17, 4099):
+        qa = rng.integers(0, 256, count).astype(np.uint8)
+        qb = rng.integers(0, 256, count).astype(np.uint8)
+        for relu in (True, False):
+            out = ops.add_relu(torch.from_numpy(qa).to(dev), 0.03, 100, torch.from_numpy(qb).to(dev),
+                               0.02, 3, 0.04, 60, relu)
+            ref = qref.add_relu_q(qa, 0.03, 100, qb, 0.02, 3, 0.04, 60, relu)
+            assert np.array_equal(out.cpu().numpy(), ref), (count, relu)
+
+
+def test_maxpool3x3s2(dev, golden_dir):
+    from qconvnet import ops
+    z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
+    out = ops.maxpool3x3s2(torch.from_numpy(z["mp_in"]).to(dev))
+    assert np.array_equal(out.cpu().numpy(), z["mp_out"])
+    q = np.random.default_rng(4).integers(0, 256, (2, 112, 112, 64)).astype(np.uint8)
+    out = ops.maxpool3x3s2(torch.from_numpy(q).to(dev))
+    assert np.array_equal(out.cpu().numpy(), qref.maxpool3x3s2_nhwc(q))
+
+
+def test_stem_pack_and_stem_conv(dev, golden_dir):
+    from qconvnet import ops
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((2, 3, 37, 41)).astype(F32)
+    s, zp = F32(0.02), 120
+    rows = ops.stem_pack(torch.from_numpy(x).to(dev), s, zp).cpu().numpy()
+    assert np.array_equal(rows, qref.stem_pack(x, s, zp))
+    # the golden 7x7/2 stem conv (torch.ao) through the packed rows
+    z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
+    i = [j for j in range(int(z["n"])) if z[f"c{j}_qx"].shape[-1] == 3][0]
+    g = lambda k: z[f"c{i}_{k}"]  # noqa: E731
+    s_x, zx = g("s_x"), int(g("zx"))
+    xf = qref.dequantize(g("qx"), s_x, zx).transpose(0, 3, 1, 2).copy()   # re-quantizes exactly
+    rows = ops.stem_pack(torch.from_numpy(xf).to(dev), s_x, zx)
+    d = _layer(dev, ops.stem_weight_rows(g("w")), s_x, g("s_w"), g("s_y"), g("b"), zx, int(g("zy")),
+               bool(g("relu")), (2, 1), (3, 0))
+    out = ops.conv(rows, zx, d).cpu().numpy()
+    assert np.array_equal(out, g("out"))
+
+
+def test_avgpool(dev):
+    from qconvnet import ops
+    q = np.random.default_rng(7).integers(0, 256, (3, 7, 7, 2048)).astype(np.uint8)
+    out = ops.avgpool(torch.from_numpy(q).to(dev), 0.05, 11, 0.03, 0).cpu().numpy()
+    assert np.array_equal(out, qref.avgpool_q(q, 0.05, 11, 0.03, 0))
+
+
+def _net(dev, layers, hw, seed):
+    from models.resnet import synthetic_images, synthetic_resnet
+    from qconvnet.resnet import quantize_resnet
+    m = synthetic_resnet(seed, layers, num_classes=1000, hw=hw, calib_images=8, device=dev)
+    calib = [torch.from_numpy(synthetic_images(8, seed + 10, hw))]
+    return m, quantize_resnet(m, calib, dev)
+
+
+@pytest.mark.parametrize("layers,hw,n", [((1, 1, 1, 1), 64, 4), ((3, 4, 6, 3), 224, 2)])
+def test_resnet_bit_exact(dev, layers, hw, n):
+    from models.resnet import synthetic_images
+    m, qm = _net(dev, layers, hw, 0)
+    x = synthetic_images(n, 99, hw)
+    logits, inter = qm.run(torch.from_numpy(x).to(dev), keep=True)
+    torch.cuda.synchronize()
+    ref, rinter = qref.resnet_int8_forward(x, qm.spec, keep=True)
+    for k in ("stem", "pool") + tuple(f"block{i}" for i in range(sum(layers))):
+        assert np.array_equal(inter[k].cpu().numpy(), rinter[k]), k
+    assert np.array_equal(logits.cpu().numpy(), ref)
+    # sanity: the int8 net tracks the fp32 net it was quantized from
+    with torch.no_grad():
+        f = m(torch.from_numpy(x).to(dev)).cpu().numpy()
+    rel = np.abs(ref - f).max() / np.abs(f).max()
+    assert rel < 0.35, rel

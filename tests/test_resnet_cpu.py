@@ -1,0 +1,61 @@
+"""CPU checks of the §8(f)2 host logic: the fp32 ResNet restatement keeps
+torchvision's state-dict layout, BN folding preserves the fp32 function, and
+the calibrated static-int8 spec run through the oracle tracks the fp32 net."""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from oracle import qref
+
+
+def _small():
+    from models.resnet import synthetic_resnet
+    return synthetic_resnet(0, (1, 1, 1, 1), num_classes=10, hw=64, calib_images=4)
+
+
+def test_resnet50_state_dict_layout():
+    from models.resnet import resnet50
+    sd = resnet50().state_dict()
+    assert len([k for k in sd if k.endswith("conv1.weight")]) == 17
+    assert sd["layer3.0.downsample.0.weight"].shape == (1024, 512, 1, 1)
+    assert sd["layer4.2.conv2.weight"].shape == (512, 512, 3, 3)
+    assert sd["fc.weight"].shape == (1000, 2048)
+    assert sum(v.numel() for k, v in sd.items() if "running" not in k and "num_batches" not in k) \
+        == 25557032   # torchvision resnet50 parameter count
+
+
+def test_fold_preserves_fp32_function():
+    from qconvnet.resnet import fold_state_dict
+    from models.resnet import synthetic_images
+    m = _small()
+    f = fold_state_dict(m.state_dict())
+    x = torch.from_numpy(synthetic_images(2, 3, 64))
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    with torch.no_grad():
+        ref = m(x)
+        y = F.max_pool2d(F.relu(F.conv2d(x, t(f["stem"][0]), t(f["stem"][1]), stride=2, padding=3)),
+                         3, 2, 1)
+        for b in f["blocks"]:
+            cv = lambda inp, k: F.conv2d(inp, t(b[k][0]), t(b[k][1]), stride=b[k][2],  # noqa: E731
+                                         padding=b[k][3])
+            o = cv(F.relu(cv(F.relu(cv(y, "c1")), "c2")), "c3")
+            y = F.relu(o + (cv(y, "ds") if "ds" in b else y))
+        y = F.linear(y.mean((2, 3)), t(f["fc"][0]), t(f["fc"][1]))
+    assert torch.allclose(y, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_static_int8_spec_tracks_fp32():
+    from qconvnet.resnet import build_spec, calibrate, fold_state_dict
+    from models.resnet import synthetic_images
+    m = _small()
+    f = fold_state_dict(m.state_dict())
+    ranges = calibrate(f, [torch.from_numpy(synthetic_images(8, 11, 64))], "cpu")
+    spec = build_spec(f, ranges, per_channel=True)
+    assert spec["stem"]["s_w"].shape == (64,) and spec["stem"]["z_y"] == 0
+    assert spec["blocks"][0]["ds"] is not None and spec["blocks"][1]["ds"] is not None
+    x = synthetic_images(4, 12, 64)
+    logits, inter = qref.resnet_int8_forward(x, spec, keep=True)
+    with torch.no_grad():
+        ref = m(torch.from_numpy(x)).numpy()
+    assert np.abs(logits - ref).max() / np.abs(ref).max() < 0.3
+    assert inter["block3"].shape == (4, 2, 2, 2048)
