@@ -158,7 +158,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--per-channel", action="store_true")
+    ap.add_argument("--workload", choices=("convnet", "resnet50"), default="convnet",
+                    help="convnet: BASELINE configs[2]/[3] (the metric); resnet50: configs[4]")
     args = ap.parse_args()
+    if args.workload == "resnet50":
+        return main_resnet(args)
 
     from qconvnet import data
     from qconvnet import dist as qd
@@ -256,6 +260,150 @@ def main():
         result["cpu_static_int8"] = cb["static_int8"]
         result["top1"] = cb["top1"]
         result["gpu_vs_cpu_ratio"] = value / cb["static_ptq"]["value"]
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ============================================================ configs[4]
+METRIC_RESNET = "images/sec at batch 512 (3×224×224) ResNet-50 bottleneck blocks, per-channel int8"
+
+
+def resnet_cpu_baseline(model_fp, seconds):
+    """torch.ao FX static int8 (fbgemm, per-channel weights) of the same
+    ResNet-50 on the host cores, and the fp32 model the reference's
+    CustomQuantizedResNet50 effectively runs (its stubs are never converted)."""
+    from torch.ao.quantization import get_default_qconfig_mapping
+    from torch.ao.quantization.quantize_fx import convert_fx, prepare_fx
+    from models.resnet import synthetic_images
+    fp = model_fp.cpu().eval()
+    threads = torch.get_num_threads()
+    xc = torch.from_numpy(synthetic_images(8, 21))
+    with torch.no_grad():
+        pq = prepare_fx(fp, get_default_qconfig_mapping("fbgemm"), example_inputs=(xc,))
+        pq(xc)
+        q = convert_fx(pq)
+    bs = 32
+    x = torch.from_numpy(synthetic_images(bs, 22))
+    out = {}
+    for name, m, budget in (("static_int8", q, seconds), ("fp32", fp, seconds / 2)):
+        with torch.no_grad():
+            m(x)
+            total, iters = 0.0, 0
+            while total < budget:
+                t0 = time.time()
+                m(x)
+                total += time.time() - t0
+                iters += 1
+        out[name] = {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
+                     "kind": "port", "sample": f"batch {bs} x {iters} iters"}
+    out["static_int8"]["sample"] = ("torch.ao FX static int8 (fbgemm, per-channel) of the same "
+                                    "ResNet-50, " + out["static_int8"]["sample"])
+    out["fp32"]["sample"] = ("fp32 ResNet-50 (what CustomQuantizedResNet50 runs: its stubs are "
+                             "never converted), " + out["fp32"]["sample"])
+    return out, q
+
+
+def main_resnet(args):
+    from models.resnet import synthetic_images, synthetic_resnet
+    from qconvnet import dist as qd
+    from qconvnet.resnet import quantize_resnet
+
+    rank, world, local = qd.init()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = args.batch if args.batch != 1024 else 512
+    fp = synthetic_resnet(0, device=dev, calib_images=32)
+    calib = [torch.from_numpy(synthetic_images(32, 1 + i)) for i in range(2)]
+    model = quantize_resnet(fp, calib, dev, per_channel=True)
+    x = torch.from_numpy(synthetic_images(B, 100 + rank)).to(dev)
+    gathered = torch.empty((world * B, model.num_classes), dtype=torch.float32,
+                           device=dev) if world > 1 else None
+
+    def step(marks=None):
+        logits = model.run(x, marks=marks)
+        if world > 1:
+            qd.gather_logits(logits, gathered)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    value = world * B * args.steps / elapsed
+
+    # MACs per image of every conv launch, in forward order
+    convs = model.conv_layers()
+    hh = (x.shape[2] + 2 * convs[0].py - convs[0].kh) // convs[0].sy + 1   # stem output
+    sizes = [hh * hh]
+    hh = (hh - 1) // 2 + 1                                                   # maxpool
+    for b in model.blocks:   # launch order: [ds], c1, c2, c3 (conv_layers())
+        ho = (hh + 2 * b["c2"].py - b["c2"].kh) // b["c2"].sy + 1
+        sizes += ([ho * ho] if b["ds"] is not None else []) + [hh * hh, ho * ho, ho * ho]
+        hh = ho
+    mac_img = [sz * d.cout * d.w.shape[0] * 32 for sz, d in zip(sizes, convs)]  # K = chunks*32
+    per_name = {}
+    n_rep = max(3, min(args.steps, 10))
+    conv_ms = []
+    for _ in range(n_rep):
+        m = []
+        step(m)
+        torch.cuda.synchronize()
+        tot_conv = 0.0
+        for (_, e0), (n1, e1) in zip(m[:-1], m[1:]):
+            ms = e0.elapsed_time(e1)
+            per_name.setdefault(n1, []).append(ms)
+            if n1 == "conv":
+                tot_conv += ms
+        conv_ms.append(tot_conv)
+    conv_ms = float(np.mean(conv_ms))
+    conv_ops = 2.0 * sum(mac_img) * B
+    tops = conv_ops / (conv_ms * 1e-3) / 1e12
+    roof = {"kernel": "conv_gen_kernel (all 53 conv launches)", "bound": "mfma", "achieved": tops,
+            "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s", "frac": tops / PEAK_INT8_TOPS, "traffic": None,
+            "note": "int8 TOPS in the TFLOP/s slot; achieved = 2*sum(conv MAC)*batch / summed "
+                    "HIP-event conv time; stem MACs counted at the packed K=224 actually issued"}
+    result = {
+        "metric": METRIC_RESNET, "value": value, "unit": "images/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic",
+        "config": {"workload": "ResNet-50 (stem, 16 bottleneck blocks, avgpool, fc) static int8, "
+                               "per-channel weights, u8 NHWC activations",
+                   "global_batch": world * B, "per_gpu_batch": B, "image": [3, 224, 224],
+                   "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "launch_ms": {k: round(float(np.sum(v) / n_rep), 4) for k, v in per_name.items()},
+        "conv_gmac_per_image": sum(mac_img) / 1e9,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb, q_cpu = resnet_cpu_baseline(fp, args.cpu_seconds)
+        result["cpu_baseline"] = cb["static_int8"]
+        result["cpu_fp32"] = cb["fp32"]
+        xe = synthetic_images(64, 31)
+        with torch.no_grad():
+            lab = fp.cpu()(torch.from_numpy(xe)).argmax(1)
+            g = model(torch.from_numpy(xe)).argmax(1)
+            c = q_cpu(torch.from_numpy(xe)).argmax(1)
+        result["top1_vs_fp32"] = {"gpu_int8": (g == lab).float().mean().item() * 100,
+                                  "cpu_torchao_int8": (c == lab).float().mean().item() * 100,
+                                  "images": 64}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -1,0 +1,363 @@
+// LDS-tiled implicit-GEMM int8 convolution for the ResNet bottleneck path
+// (SURVEY §8(f)2), with the residual join fused into the epilogue.
+//
+// D[cout][pixel] = W'[cout][k] . X'[pixel][k] on v_mfma_i32_32x32x32_i8,
+// K = (r, s, c) in 32-byte chunks.  Workgroup tile: 256 output pixels x BN
+// output channels (BN = 128, or 64 for the 64-channel convs); 4 waves, each
+// 128 x 64 (JT = 4 pixel tiles x 2 channel tiles) or 64 x 64.  K advances 64
+// bytes (two chunks) per stage through a 3-deep LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4).  Every 1-KiB piece of a stage is one fragment in
+// MFMA operand order (lane L <-> row L%32, k half L/32), so the DMA source
+// address carries the im2col gather (pixel row, tap, channel chunk) and the
+// MFMA reads are lane-linear ds_read_b128 with no bank conflicts.  Out-of-image
+// taps read a constant line of the input zero point (g_zp_lines), so padding
+// costs nothing.  Activations are biased by 0x80 after the read (u8 -> s8).
+//
+// Epilogue: FBGEMM requant (A6) per output channel, and for the last 1x1 conv
+// of a bottleneck optionally the residual join of
+// custom_quantization_model.py:94-101 in registers: y3 = requant(acc) (u8,
+// s3/z3), out = quantize(relu(s3*(y3-z3) + s_r*(r-z_r)), s_o, z_o) — the same
+// fp32 ops as qcn_add_relu_u8 on the materialised y3, so bit-identical.
+#include "common.hpp"
+#include "qconvnet_abi.hpp"
+
+namespace qcn {
+
+struct ZpLines {
+  uint8_t b[256][32];
+};
+constexpr ZpLines make_zp_lines() {
+  ZpLines z{};
+  for (int i = 0; i < 256; ++i)
+    for (int j = 0; j < 32; ++j) z.b[i][j] = (uint8_t)i;
+  return z;
+}
+// row z = 32 bytes of value z (row 0 doubles as the zero weight line)
+__device__ const ZpLines g_zp_lines = make_zp_lines();
+
+struct GemmArgs {
+  const uint8_t* x;
+  const int8_t* w;
+  int n, h, w_, cin, oh, ow, cout, kh, kw, sy, sx, py, px, x_zp;
+  long npix;
+  int kcs;     // K chunks of 32
+  int mt, nt;  // tiles along pixels / channels
+  const float *u, *v, *mult;
+  const int* corr;
+  int zp_y, lo;
+  // fused residual join (RESID): identity r (u8, s_r/z_r), y3 scale s3 (z3 = zp_y)
+  const uint8_t* r;
+  float s3, s_r, inv_o;
+  int z_r, z_o;
+  uint8_t* y;
+};
+
+template <int BN>
+struct GemmCfg {
+  static constexpr int BM = 256;
+  static constexpr int WN = BN / 64;          // waves along channels
+  static constexpr int WM = 4 / WN;           // waves along pixels
+  static constexpr int JT = BM / (32 * WM);   // pixel tiles per wave (4 or 2)
+  static constexpr int FA = 2 * BN / 32;      // A fragments (1 KiB) per stage
+  static constexpr int AREG = FA * 1024;      // A region of a stage
+  static constexpr int STAGE = AREG + BM * 64;
+  static constexpr int DA = FA / 4;           // A DMA instructions per wave per stage
+  static constexpr int D = DA + 4;            // + 4 B instructions (16 rows x 64 B each)
+  static constexpr int OS = BN + 16;          // output staging row stride (bytes)
+  static constexpr int LDS = 3 * STAGE;
+  static_assert(FA % 4 == 0, "A fragments split evenly over 4 waves");
+  static_assert(BM * OS <= LDS, "output staging fits in the ring");
+};
+
+// one K chunk (32 channels of one tap) forward in (r, s, c) order
+struct KCursor {
+  int r, s, c;
+  QCN_DEV void adv(int cin, int kw) {
+    c += 32;
+    if (c == cin) {
+      c = 0;
+      if (++s == kw) { s = 0; ++r; }
+    }
+  }
+};
+
+template <int BN, bool RESID>
+__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
+  using C = GemmCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hi = lane >> 5;
+
+  // XCD-aware tile order: consecutive tiles (same pixels, all channel tiles
+  // first) stay on one XCD's L2.
+  const int T = a.mt * a.nt;
+  const int bid = blockIdx.x, xcd = bid & 7, k8 = bid >> 3;
+  const int q = T >> 3, rm = T & 7;
+  const int t = xcd < rm ? xcd * (q + 1) + k8 : rm * (q + 1) + (xcd - rm) * q + k8;
+  const int mtile = t / a.nt, ntile = t % a.nt;
+  const long m0 = (long)mtile * C::BM;
+  const int n0 = ntile * BN;
+
+  // B (pixel) rows: a stage holds BM rows x 64 B (two K chunks); row r's 16-B
+  // piece pc sits at slot pc ^ ((r >> 2) & 3) (conflict-free MFMA reads).  DMA
+  // instruction ib covers rows 16 ib .. 16 ib + 15, lane L -> row L/4, slot L%4,
+  // so every lane loads the same piece (chunk c, half h) of its 4 rows.
+  const int bslot = lane & 3, bswz = (lane >> 4) & 3, bpc = bslot ^ bswz;
+  const int bc = bpc >> 1, bh = bpc & 1;
+  long pbase[4];
+  int iy0[4], ix0[4];
+  bool pv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long p = m0 + (wave + 4 * e) * 16 + (lane >> 2);
+    pv[e] = p < a.npix;
+    const long pc = pv[e] ? p : 0;
+    const int ox = (int)(pc % a.ow), oy = (int)((pc / a.ow) % a.oh);
+    const long img = pc / ((long)a.ow * a.oh);
+    iy0[e] = oy * a.sy - a.py;
+    ix0[e] = ox * a.sx - a.px;
+    pbase[e] = ((img * a.h + iy0[e]) * a.w_ + ix0[e]) * (long)a.cin + bh * 16;
+  }
+  const uint8_t* zpl = &g_zp_lines.b[a.x_zp][bh * 16];
+  const uint8_t* zero = &g_zp_lines.b[0][hi * 16];
+  const int8_t* wl = a.w + ((long)n0 + l32) * 32 + hi * 16;
+  const long wstep = (long)a.cout * 32;
+
+  // uniform cursors of the even and odd chunk of the next stage to load
+  KCursor cur0{0, 0, 0}, cur1{0, 0, 0};
+  cur1.adv(a.cin, a.kw);
+  const int nst = (a.kcs + 1) / 2;
+  auto issue = [&](int st) {
+    uint8_t* buf = lds + (st % 3) * C::STAGE;
+#pragma unroll
+    for (int tt = 0; tt < C::DA; ++tt) {   // A: fragment f = wave + 4 tt
+      const int f = wave + 4 * tt, c = f / (BN / 32), g = f % (BN / 32);
+      const int kc = 2 * st + c;
+      const void* src = kc < a.kcs ? (const void*)(wl + kc * wstep + g * 32 * 32) : (const void*)zero;
+      glds16(src, buf + f * 1024);
+    }
+    const int lr = bc ? cur1.r : cur0.r, ls = bc ? cur1.s : cur0.s, lc = bc ? cur1.c : cur0.c;
+    const bool live = 2 * st + bc < a.kcs;
+    const long toff = ((long)lr * a.w_ + ls) * a.cin + lc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {          // B: instruction wave + 4 e
+      const int iy = iy0[e] + lr, ix = ix0[e] + ls;
+      const bool in = live && pv[e] && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w_;
+      const void* src = in ? (const void*)(a.x + pbase[e] + toff) : (const void*)zpl;
+      glds16(src, buf + C::AREG + (wave + 4 * e) * 1024);
+    }
+    cur0.adv(a.cin, a.kw); cur0.adv(a.cin, a.kw);
+    cur1.adv(a.cin, a.kw); cur1.adv(a.cin, a.kw);
+  };
+
+  const int wc = wave % C::WN, wm = wave / C::WN;
+  v16i acc[2][C::JT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    v16i c0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int4 c4 = *reinterpret_cast<const int4*>(a.corr + n0 + wc * 64 + i * 32 + 8 * g + 4 * hi);
+      c0[4 * g] = c4.x; c0[4 * g + 1] = c4.y; c0[4 * g + 2] = c4.z; c0[4 * g + 3] = c4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < C::JT; ++j) acc[i][j] = c0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue(0);
+  if (nst > 1) issue(1);
+
+  // MFMA read offsets: A lane-linear; B row (wm*JT + j)*32 + l32, piece 2c+hi
+  const int swz = (l32 >> 2) & 3;
+  const int boff0 = C::AREG + (wm * C::JT) * 2048 + l32 * 64 + ((hi ^ swz) << 4);
+  const int boff1 = C::AREG + (wm * C::JT) * 2048 + l32 * 64 + (((2 + hi) ^ swz) << 4);
+  for (int st = 0; st < nst; ++st) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < nst) issue(st + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* buf = lds + (st % 3) * C::STAGE;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      v4i fa[2], fb[C::JT];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const v4i*>(buf + (c * (BN / 32) + wc * 2 + i) * 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < C::JT; ++j) {
+        v4i b = *reinterpret_cast<const v4i*>(buf + (c ? boff1 : boff0) + j * 2048);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) b[d] ^= (int)0x80808080u;
+        fb[j] = b;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::JT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();   // every wave is done with the ring: reuse it
+  __builtin_amdgcn_sched_barrier(0);
+
+  // Epilogue phase 1 (accumulator layout: lane (l32, hi) of tile (i, j) holds
+  // pixel l32, channels 8g + 4hi + e): FBGEMM requant to u8 — fma / mul as
+  // packed fp32 pairs, v_cvt_pk_u8_f32 (RNE + saturate) standing in for
+  // rint/+zp/clamp when zp == 0 — and dword writes into the LDS tile
+  // [BM][OS] (no lane transposes).
+  const bool fast = a.zp_y == 0;
+  const float zpf = (float)a.zp_y, lof = (float)a.lo;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int cl = wc * 64 + i * 32;   // tile's first channel within the workgroup
+    v2f u[8], v[8], mu[8];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int co = n0 + cl + 8 * g + 4 * hi;
+      const float4 x4 = *reinterpret_cast<const float4*>(a.u + co);
+      const float4 y4 = *reinterpret_cast<const float4*>(a.v + co);
+      const float4 z4 = *reinterpret_cast<const float4*>(a.mult + co);
+      u[2 * g] = (v2f){x4.x, x4.y}; u[2 * g + 1] = (v2f){x4.z, x4.w};
+      v[2 * g] = (v2f){y4.x, y4.y}; v[2 * g + 1] = (v2f){y4.z, y4.w};
+      mu[2 * g] = (v2f){z4.x, z4.y}; mu[2 * g + 1] = (v2f){z4.z, z4.w};
+    }
+#pragma unroll
+    for (int j = 0; j < C::JT; ++j) {
+      v2f ab[8];
+#pragma unroll
+      for (int h2 = 0; h2 < 8; ++h2) {
+        const v2f af = {(float)acc[i][j][2 * h2], (float)acc[i][j][2 * h2 + 1]};
+        ab[h2] = __builtin_elementwise_fma(u[h2], v[h2], af) * mu[h2];
+      }
+      uint32_t* od = reinterpret_cast<uint32_t*>(lds + ((wm * C::JT + j) * 32 + l32) * C::OS + cl) + hi;
+      if (fast) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint32_t wd = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g].x, 0, 0u);
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g].y, 1, wd);
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g + 1].x, 2, wd);
+          od[2 * g] = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g + 1].y, 3, wd);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint32_t wd = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = e & 1 ? ab[2 * g + (e >> 1)].y : ab[2 * g + (e >> 1)].x;
+            wd = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_amdgcn_fmed3f(__builtin_rintf(x) + zpf, lof, 255.0f), e, wd);
+          }
+          od[2 * g] = wd;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // Epilogue phase 2 (row-contiguous): 16 B per thread, whole 64/128-B row
+  // segments per instruction; the fused residual join reads the identity
+  // with the same coalesced pattern:
+  //   out = quantize(relu(s3*(y3-z3) + s_r*(r-z_r)), s_o, z_o)
+  constexpr int TPR = BN / 16;            // threads per row
+  constexpr int RPI = 256 / TPR;          // rows per iteration
+  const int rr = tid / TPR, cc = (tid % TPR) * 16;
+  const float z3f = (float)a.zp_y, zrf = (float)a.z_r, zof = (float)a.z_o;
+#pragma unroll 2
+  for (int r0 = 0; r0 < C::BM; r0 += RPI) {
+    const int row = r0 + rr;
+    const long p = m0 + row;
+    if (p >= a.npix) break;
+    uint4 val = *reinterpret_cast<const uint4*>(lds + row * C::OS + cc);
+    const long off = p * a.cout + n0 + cc;
+    if constexpr (RESID) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(a.r + off);
+      uint32_t yw[4] = {val.x, val.y, val.z, val.w};
+      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const v2f yf = {(float)((yw[g] >> (8 * e)) & 0xff), (float)((yw[g] >> (8 * e + 8)) & 0xff)};
+          const v2f rf = {(float)((rw[g] >> (8 * e)) & 0xff), (float)((rw[g] >> (8 * e + 8)) & 0xff)};
+          const v2f d3 = (yf - (v2f){z3f, z3f}) * (v2f){a.s3, a.s3};
+          const v2f dr = (rf - (v2f){zrf, zrf}) * (v2f){a.s_r, a.s_r};
+          const v2f sm = (d3 + dr) * (v2f){a.inv_o, a.inv_o};
+          if (a.z_o == 0) {   // ReLU is implied by the saturation at 0
+            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
+            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
+          } else {            // relu(s) * inv == max(s * inv, 0) since inv > 0
+            o = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_amdgcn_fmed3f(__builtin_rintf(fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f), e, o);
+            o = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_amdgcn_fmed3f(__builtin_rintf(fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f),
+                e + 1, o);
+          }
+        }
+        yw[g] = o;
+      }
+      val = make_uint4(yw[0], yw[1], yw[2], yw[3]);
+    }
+    *reinterpret_cast<uint4*>(a.y + off) = val;
+  }
+}
+
+template <int BN, bool RESID>
+int launch_gemm(GemmArgs& a, hipStream_t st) {
+  using C = GemmCfg<BN>;
+  a.mt = (int)((a.npix + C::BM - 1) / C::BM);
+  a.nt = a.cout / BN;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_gemm_kernel<BN, RESID>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID>), dim3(a.mt * a.nt), dim3(256), C::LDS, st, a);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+}  // namespace qcn
+
+extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                                       const int8_t* w_packed, int cout, int kh, int kw,
+                                       int stride_h, int stride_w, int pad_h, int pad_w,
+                                       const float* u, const float* v, const float* mult,
+                                       const int32_t* corr, int y_zp, int relu,
+                                       const uint8_t* resid, float y_scale, float r_scale,
+                                       int r_zp, float out_scale, int out_zp, uint8_t* y,
+                                       void* stream) {
+  if (!x || !w_packed || !u || !v || !mult || !corr || !y) return QCN_ERR_ARG;
+  if (nimg <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
+      stride_h <= 0 || stride_w <= 0 || pad_h < 0 || pad_w < 0 || x_zp < 0 || x_zp > 255 ||
+      y_zp < 0 || y_zp > 255)
+    return QCN_ERR_ARG;
+  if (resid && (!(y_scale > 0.f) || !(r_scale > 0.f) || !(out_scale > 0.f) || r_zp < 0 ||
+                r_zp > 255 || out_zp < 0 || out_zp > 255 || relu))
+    return QCN_ERR_ARG;
+  if (cin % 32 != 0 || cout % 64 != 0) return QCN_ERR_UNSUPPORTED;
+  const int oh = (h + 2 * pad_h - kh) / stride_h + 1, ow = (w + 2 * pad_w - kw) / stride_w + 1;
+  if (oh <= 0 || ow <= 0) return QCN_ERR_ARG;
+  qcn::GemmArgs a{};
+  a.x = x; a.w = w_packed;
+  a.n = nimg; a.h = h; a.w_ = w; a.cin = cin; a.oh = oh; a.ow = ow; a.cout = cout;
+  a.kh = kh; a.kw = kw; a.sy = stride_h; a.sx = stride_w; a.py = pad_h; a.px = pad_w;
+  a.x_zp = x_zp;
+  a.npix = (long)nimg * oh * ow;
+  a.kcs = kh * kw * (cin / 32);
+  a.u = u; a.v = v; a.mult = mult; a.corr = corr;
+  a.zp_y = y_zp; a.lo = relu ? y_zp : 0;
+  a.r = resid; a.s3 = y_scale; a.s_r = r_scale; a.inv_o = resid ? 1.0f / out_scale : 0.f;
+  a.z_r = r_zp; a.z_o = out_zp; a.y = y;
+  if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  if (cout % 128 == 0)
+    return resid ? qcn::launch_gemm<128, true>(a, st) : qcn::launch_gemm<128, false>(a, st);
+  return resid ? qcn::launch_gemm<64, true>(a, st) : qcn::launch_gemm<64, false>(a, st);
+}

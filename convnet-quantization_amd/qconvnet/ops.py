@@ -313,9 +313,13 @@ def stem_weight_rows(w_oihw: np.ndarray):
     return out
 
 
-def conv(x, x_zp, layer, out=None):
+def conv(x, x_zp, layer, out=None, resid=None, impl=None):
     """Generic quantized conv on u8 NHWC.  ``layer`` carries w (packed), cout,
-    kh, kw, stride (sy, sx), pad (py, px), u, v, mult, corr, z_y, relu."""
+    kh, kw, stride (sy, sx), pad (py, px), u, v, mult, corr, z_y, s_y, relu.
+    ``resid=(r, s_r, z_r, s_out, z_out)`` fuses the bottleneck's residual join
+    (GEMM kernel only).  impl: "gemm" (LDS-tiled, default) or "gen" (the
+    register-direct kernel; QCN_CONV_IMPL overrides the default)."""
+    import os
     _need(x, torch.uint8, "conv.x")
     n, h, w, cin = x.shape
     d = layer
@@ -323,10 +327,26 @@ def conv(x, x_zp, layer, out=None):
     ow = (w + 2 * d.px - d.kw) // d.sx + 1
     if out is None:
         out = torch.empty((n, oh, ow, d.cout), dtype=torch.uint8, device=x.device)
-    check(lib().qcn_conv_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, d.kh, d.kw,
-                                   d.sy, d.sx, d.py, d.px, _ptr(d.u), _ptr(d.v), _ptr(d.mult),
-                                   _ptr(d.corr), int(d.z_y), int(bool(d.relu)), _ptr(out),
-                                   _stream()), "conv")
+    impl = impl or os.environ.get("QCN_CONV_IMPL", "gemm")
+    if impl == "gen" and resid is None:
+        check(lib().qcn_conv_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, d.kh,
+                                       d.kw, d.sy, d.sx, d.py, d.px, _ptr(d.u), _ptr(d.v),
+                                       _ptr(d.mult), _ptr(d.corr), int(d.z_y), int(bool(d.relu)),
+                                       _ptr(out), _stream()), "conv")
+        return out
+    if resid is not None:
+        r, s_r, z_r, s_o, z_o = resid
+        _need(r, torch.uint8, "conv.resid")
+        if tuple(r.shape) != tuple(out.shape):
+            raise ValueError("residual operand shape differs from the conv output")
+        rp, sy_ = _ptr(r), float(d.s_y)
+    else:
+        rp, sy_, s_r, z_r, s_o, z_o = None, 0.0, 0.0, 0, 0.0, 0
+    check(lib().qcn_conv_gemm_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, d.kh,
+                                        d.kw, d.sy, d.sx, d.py, d.px, _ptr(d.u), _ptr(d.v),
+                                        _ptr(d.mult), _ptr(d.corr), int(d.z_y), int(bool(d.relu)),
+                                        rp, sy_, float(s_r), int(z_r), float(s_o), int(z_o),
+                                        _ptr(out), _stream()), "conv_gemm")
     return out
 
 

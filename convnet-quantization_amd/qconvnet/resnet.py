@@ -19,6 +19,7 @@ kernel on the current stream, capturable into a HIP graph):
 """
 from __future__ import annotations
 
+import os
 import re
 
 import numpy as np
@@ -212,7 +213,7 @@ class QuantizedResNet:
         """Every conv launch in forward order (for MAC accounting)."""
         out = [self.stem]
         for b in self.blocks:
-            out += [b["c1"], b["c2"], b["c3"]] + ([b["ds"]] if b["ds"] is not None else [])
+            out += ([b["ds"]] if b["ds"] is not None else []) + [b["c1"], b["c2"], b["c3"]]
         return out
 
     def run(self, x, keep=False, marks=None):
@@ -235,23 +236,28 @@ class QuantizedResNet:
         mark("maxpool")
         if keep:
             inter["stem"] = q
+        fuse = os.environ.get("QCN_RESID_FUSED", "1") == "1"
         for i, (b, e) in enumerate(zip(self.blocks, sp["blocks"])):
             zx = b["c1"].z_x
-            y = ops.conv(q, zx, b["c1"])
-            mark("conv")
-            y = ops.conv(y, b["c2"].z_x, b["c2"])
-            mark("conv")
-            y = ops.conv(y, b["c3"].z_x, b["c3"])
-            mark("conv")
-            if b["ds"] is not None:
+            if b["ds"] is not None:   # identity first, so conv3 can consume it
                 idn = ops.conv(q, zx, b["ds"])
                 mark("conv")
                 si, zi = e["ds"]["s_y"], e["ds"]["z_y"]
             else:
                 idn, si, zi = q, e["c1"]["s_x"], zx
+            y = ops.conv(q, zx, b["c1"])
+            mark("conv")
+            y = ops.conv(y, b["c2"].z_x, b["c2"])
+            mark("conv")
             so, zo = e["out"]
-            q = ops.add_relu(y, e["c3"]["s_y"], e["c3"]["z_y"], idn, si, zi, so, zo, True)
-            mark("add")
+            if fuse:   # conv3 + residual join in one launch
+                q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
+                mark("conv")
+            else:
+                y = ops.conv(y, b["c3"].z_x, b["c3"])
+                mark("conv")
+                q = ops.add_relu(y, e["c3"]["s_y"], e["c3"]["z_y"], idn, si, zi, so, zo, True)
+                mark("add")
             if keep:
                 inter[f"block{i}"] = q
         last = sp["blocks"][-1]["out"] if sp["blocks"] else (sp["stem"]["s_y"], sp["stem"]["z_y"])

@@ -205,6 +205,18 @@ int qcn_conv_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_
                        int stride_w, int pad_h, int pad_w, const float* u, const float* v,
                        const float* mult, const int32_t* corr, int y_zp, int relu, uint8_t* y,
                        void* stream);
+/* Same conv as qcn_conv_u8s8_nhwc on the LDS-tiled implicit-GEMM kernel
+ * (256-pixel x 128/64-channel tiles, LDS-DMA im2col).  With resid != NULL the
+ * residual join is fused into the epilogue (the conv must have relu == 0):
+ * y3 = requant(acc) with (y_scale, y_zp), then
+ * y = quantize(relu(y_scale*(y3-y_zp) + r_scale*(resid-r_zp)), out_scale, out_zp)
+ * — bit-identical to qcn_conv_u8s8_nhwc followed by qcn_add_relu_u8. */
+int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                            const int8_t* w_packed, int cout, int kh, int kw, int stride_h,
+                            int stride_w, int pad_h, int pad_w, const float* u, const float* v,
+                            const float* mult, const int32_t* corr, int y_zp, int relu,
+                            const uint8_t* resid, float y_scale, float r_scale, int r_zp,
+                            float out_scale, int out_zp, uint8_t* y, void* stream);
 /* Residual join (custom_quantization_model.py:94-101 then the next stage's
  * QuantStub): y = quantize(relu?(fp32(sa*(a-za)) + fp32(sb*(b-zb))), s_out, z_out). */
 int qcn_add_relu_u8(const uint8_t* a, float sa, int za, const uint8_t* b, float sb, int zb,

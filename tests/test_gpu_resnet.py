@@ -41,7 +41,8 @@ def _layer(dev, w_oihw, s_x, s_w, s_y, b, z_x, z_y, relu, stride, pad):
     return d
 
 
-def test_conv_general_golden(dev, golden_dir):
+@pytest.mark.parametrize("impl", ["gemm", "gen"])
+def test_conv_general_golden(dev, golden_dir, impl):
     from qconvnet import ops
     z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
     ran = 0
@@ -52,7 +53,7 @@ def test_conv_general_golden(dev, golden_dir):
         st, pd = int(g("stride")), int(g("pad"))
         d = _layer(dev, g("w"), g("s_x"), g("s_w"), g("s_y"), g("b"), int(g("zx")), int(g("zy")),
                    bool(g("relu")), (st, st), (pd, pd))
-        out = ops.conv(torch.from_numpy(g("qx")).to(dev), int(g("zx")), d)
+        out = ops.conv(torch.from_numpy(g("qx")).to(dev), int(g("zx")), d, impl=impl)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), g("out")), i
         ran += 1
@@ -66,8 +67,11 @@ def test_conv_general_golden(dev, golden_dir):
     (2, 14, 14, 256, 512, 1, 1, 2, 0, 4, False, 128, True),
     (5, 9, 6, 32, 64, 3, 3, 1, 1, 255, True, 0, False),
     (1, 1, 1, 64, 128, 3, 3, 1, 1, 13, True, 0, True),
+    (2, 56, 56, 64, 64, 3, 3, 1, 1, 0, True, 0, True),
+    (1, 28, 28, 128, 512, 1, 1, 1, 0, 9, False, 140, True),
 ])
-def test_conv_general_oracle(dev, shape):
+@pytest.mark.parametrize("impl", ["gemm", "gen"])
+def test_conv_general_oracle(dev, shape, impl):
     from qconvnet import ops
     n, h, w, cin, cout, kh, kw, st, pd, zx, relu, zy, pc = shape
     rng = np.random.default_rng(hash(shape) & 0xffff)
@@ -79,12 +83,18 @@ def test_conv_general_oracle(dev, shape):
     b = (rng.standard_normal(cout) * 0.3).astype(F32)
     s_x, s_y = F32(0.02), F32(0.9 if cin >= 256 else 0.2)
     d = _layer(dev, wq, s_x, s_w, s_y, b, zx, zy, relu, (st, st), (pd, pd))
-    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d).cpu().numpy()
+    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d, impl=impl).cpu().numpy()
     u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
     ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, relu, (st, st), (pd, pd))
     assert out.shape == ref.shape
     assert np.array_equal(out, ref)
     assert len(np.unique(ref)) > 8, "degenerate case"
+    if not relu:   # the fused residual join equals conv -> add_relu
+        d.s_y = s_y
+        r = rng.integers(0, 256, ref.shape).astype(np.uint8)
+        fused = ops.conv(torch.from_numpy(qx).to(dev), zx, d,
+                         resid=(torch.from_numpy(r).to(dev), F32(0.03), 17, F32(0.05), 0)).cpu().numpy()
+        assert np.array_equal(fused, qref.add_relu_q(ref, s_y, zy, r, F32(0.03), 17, F32(0.05), 0))
 
 
 def test_add_relu_golden_and_ragged(dev, golden_dir):
