@@ -375,7 +375,7 @@ def main_resnet(args):
     conv_ms = float(np.mean(conv_ms))
     conv_ops = 2.0 * sum(mac_img) * B
     tops = conv_ops / (conv_ms * 1e-3) / 1e12
-    roof = {"kernel": "conv_gen_kernel (all 53 conv launches)", "bound": "mfma", "achieved": tops,
+    roof = {"kernel": "conv_gemm_kernel (all 53 conv launches)", "bound": "mfma", "achieved": tops,
             "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s", "frac": tops / PEAK_INT8_TOPS, "traffic": None,
             "note": "int8 TOPS in the TFLOP/s slot; achieved = 2*sum(conv MAC)*batch / summed "
                     "HIP-event conv time; stem MACs counted at the packed K=224 actually issued"}

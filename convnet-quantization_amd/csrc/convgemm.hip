@@ -21,6 +21,8 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
+#include <type_traits>
+
 namespace qcn {
 
 struct ZpLines {
@@ -205,6 +207,99 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   __builtin_amdgcn_s_barrier();   // every wave is done with the ring: reuse it
   __builtin_amdgcn_sched_barrier(0);
 
+  if constexpr (RESID) {
+    // Residual join: per channel half i, phase 1 writes the dequantized conv
+    // output d3 = s3*(y3 - z3) as fp32 — y3 - z3 = med3(rint(ab), -z3, 255-z3)
+    // exactly (conv3 has no ReLU), so the u8 y3 is never materialised — into
+    // an LDS tile [BM][32*WN floats]; phase 2 reads it row-contiguous next to
+    // the coalesced identity bytes: out = quantize(relu(d3 + s_r*(r - z_r))).
+    constexpr int NCOL = 32 * C::WN;           // local columns per half
+    constexpr int OSF = NCOL * 4 + 16;         // fp32 row stride (bytes)
+    constexpr int TPR = NCOL / 16, RPI = 256 / TPR;
+    static_assert(C::BM * OSF <= C::LDS, "fp32 staging fits in the ring");
+    const v2f nz3 = {-(float)a.zp_y, -(float)a.zp_y}, hz3 = {255.0f - a.zp_y, 255.0f - a.zp_y};
+    const v2f s3 = {a.s3, a.s3};
+    const int rr = tid / TPR, cq = tid % TPR;   // phase-2 row / 16-column group
+    const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co0 = n0 + wc * 64 + i * 32;
+      v2f u[8], v[8], mu[8];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int co = co0 + 8 * g + 4 * hi;
+        const float4 x4 = *reinterpret_cast<const float4*>(a.u + co);
+        const float4 y4 = *reinterpret_cast<const float4*>(a.v + co);
+        const float4 z4 = *reinterpret_cast<const float4*>(a.mult + co);
+        u[2 * g] = (v2f){x4.x, x4.y}; u[2 * g + 1] = (v2f){x4.z, x4.w};
+        v[2 * g] = (v2f){y4.x, y4.y}; v[2 * g + 1] = (v2f){y4.z, y4.w};
+        mu[2 * g] = (v2f){z4.x, z4.y}; mu[2 * g + 1] = (v2f){z4.z, z4.w};
+      }
+#pragma unroll
+      for (int j = 0; j < C::JT; ++j) {
+        uint8_t* rowp = lds + ((wm * C::JT + j) * 32 + l32) * OSF + (wc * 32) * 4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          v2f d[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int h2 = 2 * g + h;
+            const v2f af = {(float)acc[i][j][2 * h2], (float)acc[i][j][2 * h2 + 1]};
+            const v2f ab = __builtin_elementwise_fma(u[h2], v[h2], af) * mu[h2];
+            d[h] = (v2f){__builtin_amdgcn_fmed3f(__builtin_rintf(ab.x), nz3.x, hz3.x),
+                         __builtin_amdgcn_fmed3f(__builtin_rintf(ab.y), nz3.x, hz3.x)} * s3;
+          }
+          *reinterpret_cast<float4*>(rowp + (8 * g + 4 * hi) * 4) = make_float4(d[0].x, d[0].y, d[1].x, d[1].y);
+        }
+      }
+      __syncthreads();
+      const v2f zr = {(float)a.z_r, (float)a.z_r}, sr = {a.s_r, a.s_r}, io = {a.inv_o, a.inv_o};
+      const float zof = (float)a.z_o;
+      auto join = [&](auto zo0) {
+        constexpr bool ZO0 = decltype(zo0)::value;   // z_o == 0: ReLU = saturation at 0
+#pragma unroll 2
+        for (int r0 = 0; r0 < C::BM; r0 += RPI) {
+          const int row = r0 + rr;
+          const long p = m0 + row;
+          if (p >= a.npix) break;
+          const long off = p * a.cout + ch2 + 32 * i;
+          const uint4 rv = *reinterpret_cast<const uint4*>(a.r + off);
+          const float4* dp = reinterpret_cast<const float4*>(lds + row * OSF + cq * 64);
+          const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+          uint32_t ow[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 d4 = dp[g];
+            uint32_t o = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+              const v2f rf = {(float)((rw[g] >> (8 * e)) & 0xff), (float)((rw[g] >> (8 * e + 8)) & 0xff)};
+              const v2f dd = e ? (v2f){d4.z, d4.w} : (v2f){d4.x, d4.y};
+              const v2f sm = (dd + (rf - zr) * sr) * io;
+              if constexpr (ZO0) {
+                o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
+                o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
+              } else {   // relu(s) * inv == max(s * inv, 0) since inv > 0
+                o = __builtin_amdgcn_cvt_pk_u8_f32(
+                    __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f),
+                    e, o);
+                o = __builtin_amdgcn_cvt_pk_u8_f32(
+                    __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f),
+                    e + 1, o);
+              }
+            }
+            ow[g] = o;
+          }
+          *reinterpret_cast<uint4*>(a.y + off) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+      };
+      if (a.z_o == 0) join(std::true_type{});
+      else join(std::false_type{});
+      __syncthreads();
+    }
+    return;
+  }
+
   // Epilogue phase 1 (accumulator layout: lane (l32, hi) of tile (i, j) holds
   // pixel l32, channels 8g + 4hi + e): FBGEMM requant to u8 — fma / mul as
   // packed fp32 pairs, v_cvt_pk_u8_f32 (RNE + saturate) standing in for
@@ -261,50 +356,17 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   __syncthreads();
 
   // Epilogue phase 2 (row-contiguous): 16 B per thread, whole 64/128-B row
-  // segments per instruction; the fused residual join reads the identity
-  // with the same coalesced pattern:
-  //   out = quantize(relu(s3*(y3-z3) + s_r*(r-z_r)), s_o, z_o)
+  // segments per store instruction.
   constexpr int TPR = BN / 16;            // threads per row
   constexpr int RPI = 256 / TPR;          // rows per iteration
   const int rr = tid / TPR, cc = (tid % TPR) * 16;
-  const float z3f = (float)a.zp_y, zrf = (float)a.z_r, zof = (float)a.z_o;
 #pragma unroll 2
   for (int r0 = 0; r0 < C::BM; r0 += RPI) {
     const int row = r0 + rr;
     const long p = m0 + row;
     if (p >= a.npix) break;
-    uint4 val = *reinterpret_cast<const uint4*>(lds + row * C::OS + cc);
-    const long off = p * a.cout + n0 + cc;
-    if constexpr (RESID) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(a.r + off);
-      uint32_t yw[4] = {val.x, val.y, val.z, val.w};
-      const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const v2f yf = {(float)((yw[g] >> (8 * e)) & 0xff), (float)((yw[g] >> (8 * e + 8)) & 0xff)};
-          const v2f rf = {(float)((rw[g] >> (8 * e)) & 0xff), (float)((rw[g] >> (8 * e + 8)) & 0xff)};
-          const v2f d3 = (yf - (v2f){z3f, z3f}) * (v2f){a.s3, a.s3};
-          const v2f dr = (rf - (v2f){zrf, zrf}) * (v2f){a.s_r, a.s_r};
-          const v2f sm = (d3 + dr) * (v2f){a.inv_o, a.inv_o};
-          if (a.z_o == 0) {   // ReLU is implied by the saturation at 0
-            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
-            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
-          } else {            // relu(s) * inv == max(s * inv, 0) since inv > 0
-            o = __builtin_amdgcn_cvt_pk_u8_f32(
-                __builtin_amdgcn_fmed3f(__builtin_rintf(fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f), e, o);
-            o = __builtin_amdgcn_cvt_pk_u8_f32(
-                __builtin_amdgcn_fmed3f(__builtin_rintf(fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f),
-                e + 1, o);
-          }
-        }
-        yw[g] = o;
-      }
-      val = make_uint4(yw[0], yw[1], yw[2], yw[3]);
-    }
-    *reinterpret_cast<uint4*>(a.y + off) = val;
+    *reinterpret_cast<uint4*>(a.y + p * a.cout + n0 + cc) =
+        *reinterpret_cast<const uint4*>(lds + row * C::OS + cc);
   }
 }
 
