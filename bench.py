@@ -61,14 +61,16 @@ HBM_BOUND = {"conv1"}
 
 
 def build_model(rank, device, per_channel=False):
-    from models.baseline_model import synthetic_model
+    from models.baseline_model import trained_synthetic_model
     from qconvnet import data
     from qconvnet.dist import broadcast_object
     from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
     payload = None
     if rank == 0:
-        calib = torch.from_numpy(data.synthetic_images(512, 1))
-        fp = synthetic_model(0, calib)
+        # trained on the synthetic 10-class task (no CIFAR-10 / checkpoint offline)
+        x_cal, _ = data.synthetic_task(512, 1)
+        calib = torch.from_numpy(x_cal)
+        fp = trained_synthetic_model(0, device=device)
         folded = fold_state_dict(fp.state_dict())
         ranges = calibrate(folded, [calib], "cpu")
         payload = (build_qspec(folded, ranges, "static", per_channel), fp.state_dict())
@@ -106,7 +108,7 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
                                    f"batch {bs} x {iters} iters, time.time() loop as "
                                    f"utils/inference_benchmark.py:92-100"}
     # (2) full static int8 on the CPU (torch.ao eager, fbgemm) — apples to apples
-    calib = torch.from_numpy(data.synthetic_images(512, 1))
+    calib = torch.from_numpy(data.synthetic_task(512, 1)[0])   # the GPU model's calibration set
     q = torch_ref.build_static_int8_cpu(fp, [calib])
     bs2 = 256
     x2 = torch.from_numpy(data.synthetic_images(bs2, 12))
@@ -121,13 +123,15 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
     out["static_int8"] = {"value": bs2 * iters / total, "unit": "images/sec", "cores": threads,
                           "kind": "port",
                           "sample": f"torch.ao eager static int8 (fbgemm), batch {bs2} x {iters} iters"}
-    # (3) top-1 agreement on 1024 synthetic images (labels = fp32 argmax: no CIFAR offline)
-    xe = torch.from_numpy(data.synthetic_images(1024, 13))
+    # (3) top-1 on a held-out synthetic test set with true labels (the fp32
+    #     model was trained on the same task; CIFAR-10 is not available offline)
+    xe_np, ye_np = data.synthetic_task(4096, 77)
+    xe, lab = torch.from_numpy(xe_np), torch.from_numpy(ye_np)
     with torch.no_grad():
-        lab = fp(xe).argmax(1)
-        ref_top1 = (sp(xe).argmax(1) == lab).float().mean().item() * 100
-        gpu_top1 = (qmodel_gpu(xe).argmax(1) == lab).float().mean().item() * 100
-        cpu_int8_top1 = (q(xe).argmax(1) == lab).float().mean().item() * 100
+        fp_pred = fp(xe).argmax(1)
+        ref_pred = sp(xe).argmax(1)
+        gpu_pred = qmodel_gpu(xe).argmax(1)
+        cpu_int8_pred = q(xe).argmax(1)
     # the reference's own StaticPTQModel semantics on the GPU (fp32 convs +
     # HIP dynamic int8 Linear, models/static_ptq_model.py mode="reference")
     from models.static_ptq_model import StaticPTQModel
@@ -135,17 +139,21 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
     rm.load_state_dict(state_dict)
     rq = rm.quantize()
     with torch.no_grad():
-        gpu_ref_top1 = (rq(xe.to(qmodel_gpu.device)).argmax(1).cpu() == lab).float().mean().item() * 100
-    out["top1"] = {"labels": "fp32 SimpleConvNet argmax on 1024 synthetic images",
-                   "gpu_int8_static": gpu_top1, "cpu_reference_static_ptq": ref_top1,
-                   "cpu_torchao_static_int8": cpu_int8_top1,
-                   "gpu_reference_mode_static_ptq": gpu_ref_top1,
-                   "delta_vs_reference_pct": gpu_top1 - ref_top1,
-                   "delta_reference_mode_pct": gpu_ref_top1 - ref_top1,
-                   "note": "full static int8 agrees with torch.ao/fbgemm static int8 exactly "
-                           "(identical logits); the gap to the reference StaticPTQModel "
-                           "(dynamic int8 Linear only, fp32 convs) is the cost of quantizing "
-                           "the convs on this random-weight synthetic model"}
+        gpu_ref_pred = rq(xe.to(qmodel_gpu.device)).argmax(1).cpu()
+
+    def acc(p):
+        return (p == lab).float().mean().item() * 100
+
+    out["top1"] = {"labels": "true labels of 4096 held-out images of the synthetic 10-class task "
+                             "the fp32 SimpleConvNet was trained on (qconvnet.data.synthetic_task)",
+                   "fp32": acc(fp_pred), "gpu_int8_static": acc(gpu_pred),
+                   "cpu_reference_static_ptq": acc(ref_pred),
+                   "cpu_torchao_static_int8": acc(cpu_int8_pred),
+                   "gpu_reference_mode_static_ptq": acc(gpu_ref_pred),
+                   "delta_vs_reference_pct": acc(gpu_pred) - acc(ref_pred),
+                   "delta_reference_mode_pct": acc(gpu_ref_pred) - acc(ref_pred),
+                   "gpu_int8_equals_torchao_static_int8": bool(torch.equal(gpu_pred, cpu_int8_pred)),
+                   "agreement_gpu_int8_vs_fp32_pct": (gpu_pred == fp_pred).float().mean().item() * 100}
     return out
 
 

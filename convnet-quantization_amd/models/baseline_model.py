@@ -94,6 +94,30 @@ def synthetic_model(seed=0, calib_images=None):
     return model.eval()
 
 
+def trained_synthetic_model(seed=0, steps=400, batch=256, device="cuda", lr=2e-3):
+    """SimpleConvNet trained on the synthetic 10-class task
+    (qconvnet.data.synthetic_task) — a bench/test fixture standing in for the
+    reference's trained CIFAR-10 checkpoint (model_trainer.py), which is not
+    available offline.  A trained net has real decision margins, so top-1
+    deltas between quantization schemes mean what they mean on CIFAR-10."""
+    from qconvnet import data
+    torch.manual_seed(seed)
+    dev = torch.device(device)
+    model = SimpleConvNet().to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, steps)
+    model.train()
+    for it in range(steps):
+        x, y = data.synthetic_task(batch, 10_000 + seed * 100_003 + it)
+        x, y = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+        loss = torch.nn.functional.cross_entropy(model(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        sched.step()
+    return model.eval().cpu()
+
+
 def test_model():
     model = SimpleConvNet()
     y = model(torch.randn(1, 3, 32, 32))

@@ -1,5 +1,6 @@
 """CustomQuantizationModel — drop-in for
-/root/reference/models/custom_quantization_model.py:145-261 (BASELINE config 2).
+/root/reference/models/custom_quantization_model.py:145-261 (BASELINE config 2),
+and CustomQuantizedResNet50 (:104-148, config 5) below.
 
 Reference behaviour: engine select (fbgemm, else qnnpack, else RuntimeError,
 :155-161); load_state_dict (:163-167); quantize() = eval -> cpu ->
@@ -77,6 +78,45 @@ class CustomQuantizationModel:
 
     def state_dict(self):
         return self.model.state_dict()
+
+
+class CustomQuantizedResNet50:
+    """Drop-in for CustomQuantizedResNet50
+    (/root/reference/models/custom_quantization_model.py:104-148): wraps a
+    torchvision-layout ResNet (models.resnet.resnet50 or a torchvision model) —
+    stem conv + maxpool, the CustomQuantizedBottleneck blocks (:60-102) with
+    their float-domain residual add, avgpool and fc — as the static int8
+    MI355X executor ``qconvnet.resnet.QuantizedResNet`` (BN folded, per-channel
+    s8 weights, MinMax-calibrated u8 activations).  ``calibration_batches``:
+    an iterable of fp32 [N,3,H,W] tensors (or (x, y) pairs); default 32
+    synthetic ImageNet-normalised 224x224 images.  ``conv1_scale`` is accepted
+    for signature compatibility; the reference never uses it."""
+
+    def __init__(self, model, conv1_scale=1.0, calibration_batches=None, device="cuda",
+                 per_channel=True):
+        from qconvnet.resnet import quantize_resnet
+        from models.resnet import synthetic_images
+        if calibration_batches is None:
+            calibration_batches = [torch.from_numpy(synthetic_images(32, 1))]
+        batches = [b[0] if isinstance(b, (tuple, list)) else b for b in calibration_batches]
+        self.conv1_scale = conv1_scale
+        self.quantized_model = quantize_resnet(model.eval(), batches, device, per_channel)
+
+    def __call__(self, x):
+        return self.quantized_model(x)
+
+    forward = __call__
+
+    def eval(self):
+        return self
+
+    def to(self, device):
+        self.quantized_model.to(device)
+        return self
+
+    def cpu(self):
+        self.quantized_model.cpu()
+        return self
 
 
 def test_custom_quantization():

@@ -22,6 +22,34 @@ def synthetic_images(n, seed, hw=32, mean=CIFAR_MEAN, std=CIFAR_STD):
     return ((u - m) / s).astype(np.float32)
 
 
+def _class_templates(hw=32, k=10, seed=1234):
+    """k fixed smooth colour patterns (8x8 noise upsampled) — the class means
+    of the synthetic task."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    low = rng.standard_normal((k, 3, 8, 8)).astype(np.float32)
+    t = np.repeat(np.repeat(low, hw // 8, axis=2), hw // 8, axis=3)
+    return t
+
+
+def synthetic_task(n, seed, hw=32, noise=1.3):
+    """A learnable 10-class CIFAR-shaped task (CIFAR-10 is not on disk):
+    x = template[y] * contrast + smooth clutter + pixel noise, randomly
+    flipped, squashed to [0,1] and CIFAR-normalised.  Returns (x, y) numpy."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    t = _class_templates(hw)
+    y = rng.integers(0, 10, n)
+    contrast = rng.uniform(0.5, 1.5, (n, 1, 1, 1)).astype(np.float32)
+    clutter = np.repeat(np.repeat(rng.standard_normal((n, 3, hw // 4, hw // 4)).astype(np.float32),
+                                  4, axis=2), 4, axis=3)
+    x = t[y] * contrast + noise * clutter + 0.5 * rng.standard_normal((n, 3, hw, hw)).astype(np.float32)
+    flip = rng.random(n) < 0.5
+    x[flip] = x[flip][..., ::-1]
+    u = 1.0 / (1.0 + np.exp(-0.7 * x))
+    m = np.asarray(CIFAR_MEAN, np.float32).reshape(1, 3, 1, 1)
+    s = np.asarray(CIFAR_STD, np.float32).reshape(1, 3, 1, 1)
+    return ((u - m) / s).astype(np.float32), y.astype(np.int64)
+
+
 def calibration_batches(loader=None, max_batches=None, default_images=512, default_seed=1):
     """Images from a reference-style loader ((images, labels) batches), a
     tensor, or — when None — the first 512 synthetic images of seed 1."""

@@ -178,3 +178,21 @@ def test_resnet_bit_exact(dev, layers, hw, n):
         f = m(torch.from_numpy(x).to(dev)).cpu().numpy()
     rel = np.abs(ref - f).max() / np.abs(f).max()
     assert rel < 0.35, rel
+
+
+def test_custom_quantized_resnet50_wrapper(dev):
+    """The models.custom_quantization_model drop-in builds the same executor."""
+    from models.custom_quantization_model import CustomQuantizedResNet50
+    from models.resnet import synthetic_images, synthetic_resnet
+    from qconvnet.resnet import quantize_resnet
+    m = synthetic_resnet(1, (1, 1, 1, 1), num_classes=10, hw=64, calib_images=8, device=dev)
+    calib = [torch.from_numpy(synthetic_images(8, 5, 64))]
+    w = CustomQuantizedResNet50(m, calibration_batches=[(calib[0], None)], device=dev)
+    x = synthetic_images(3, 6, 64)
+    out = w(torch.from_numpy(x))
+    assert out.shape == (3, 10) and out.device.type == "cpu"
+    # (MIOpen's fp32 calibration convs may pick different algorithms per call,
+    # so the wrapper is checked against the oracle on its own spec)
+    ref, _ = qref.resnet_int8_forward(x, w.quantized_model.spec)
+    assert np.array_equal(out.numpy(), ref)
+    assert isinstance(w.quantized_model, type(quantize_resnet(m, calib, dev)))
