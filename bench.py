@@ -166,6 +166,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--per-channel", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the forward as one HIP graph (measured: no gain, the launch "
+                         "queue already runs back to back)")
     ap.add_argument("--workload", choices=("convnet", "resnet50"), default="convnet",
                     help="convnet: BASELINE configs[2]/[3] (the metric); resnet50: configs[4]")
     args = ap.parse_args()
@@ -186,8 +189,15 @@ def main():
     x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
     gathered = torch.empty((world * B, 10), dtype=torch.float32, device=dev) if world > 1 else None
 
+    use_graph = args.graph
+    if use_graph:   # the forward's launches as one HIP graph (same kernels, no launch gaps)
+        model.capture_graph(x)
+
     def step(marks=None):
-        logits = model.run(x, marks=marks)
+        if marks is None and use_graph:
+            logits = model.replay(B)
+        else:
+            logits = model.run(x, marks=marks)
         if world > 1:
             qd.gather_logits(logits, gathered)
 
@@ -330,8 +340,15 @@ def main_resnet(args):
     gathered = torch.empty((world * B, model.num_classes), dtype=torch.float32,
                            device=dev) if world > 1 else None
 
+    use_graph = args.graph
+    if use_graph:   # the forward's launches as one HIP graph (same kernels, no launch gaps)
+        model.capture_graph(x)
+
     def step(marks=None):
-        logits = model.run(x, marks=marks)
+        if marks is None and use_graph:
+            logits = model.replay(B)
+        else:
+            logits = model.run(x, marks=marks)
         if world > 1:
             qd.gather_logits(logits, gathered)
 
