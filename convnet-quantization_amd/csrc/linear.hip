@@ -283,21 +283,25 @@ int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, i
 
 long long qcn_linear_dynamic_workspace_size(int m, int k) { return 64 + (long long)m * k; }
 
-int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
-                           const float* w_scale, int per_channel, const int32_t* wsum,
-                           const float* bias, int reduce_range, float* y, void* workspace,
-                           void* stream) {
+static int linear_dynamic_impl(const float* x, int m, int k, const int8_t* w, int n,
+                               const float* w_scale, int per_channel, const int32_t* wsum,
+                               const float* bias, int reduce_range, const float* ext_minmax,
+                               float* y, void* workspace, void* stream) {
   if (!x || !w || !w_scale || !wsum || !y || !workspace) return QCN_ERR_ARG;
   if (m <= 0 || k <= 0 || n <= 0) return QCN_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   float* mm = reinterpret_cast<float*>(workspace);
   float* dyn = mm + 4;
   uint8_t* qx = reinterpret_cast<uint8_t*>(workspace) + 64;
-  int rc = qcn_minmax_reset(mm, stream);
-  if (rc) return rc;
-  rc = qcn_minmax_f32(x, (long long)m * k, mm, stream);
-  if (rc) return rc;
-  hipLaunchKernelGGL(qcn::choose_qparams_kernel, dim3(1), dim3(64), 0, st, mm, reduce_range, dyn);
+  const float* range = ext_minmax;
+  if (!range) {   // this batch's own [min, max]
+    int rc = qcn_minmax_reset(mm, stream);
+    if (rc) return rc;
+    rc = qcn_minmax_f32(x, (long long)m * k, mm, stream);
+    if (rc) return rc;
+    range = mm;
+  }
+  hipLaunchKernelGGL(qcn::choose_qparams_kernel, dim3(1), dim3(64), 0, st, range, reduce_range, dyn);
   const long long cnt = (long long)m * k;
   int g = (int)((cnt + 255) / 256 < 2048 ? (cnt + 255) / 256 : 2048);
   hipLaunchKernelGGL(qcn::quantize_legacy_kernel, dim3(g), dim3(256), 0, st, x, cnt, dyn, qx);
@@ -313,6 +317,23 @@ int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
                        w, n, ep, nullptr, y);
   }
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
+                           const float* w_scale, int per_channel, const int32_t* wsum,
+                           const float* bias, int reduce_range, float* y, void* workspace,
+                           void* stream) {
+  return linear_dynamic_impl(x, m, k, w, n, w_scale, per_channel, wsum, bias, reduce_range,
+                             nullptr, y, workspace, stream);
+}
+
+int qcn_linear_dynamic_range_f32(const float* x, int m, int k, const int8_t* w, int n,
+                                 const float* w_scale, int per_channel, const int32_t* wsum,
+                                 const float* bias, int reduce_range, const float* minmax,
+                                 float* y, void* workspace, void* stream) {
+  if (!minmax) return QCN_ERR_ARG;
+  return linear_dynamic_impl(x, m, k, w, n, w_scale, per_channel, wsum, bias, reduce_range,
+                             minmax, y, workspace, stream);
 }
 
 int qcn_linear_f32(const float* x, int m, int k, const float* w, int n, const float* b,

@@ -38,6 +38,7 @@ class DynamicQuantConvNet:
     def __init__(self, state_dict, fold=True, device="cuda", reduce_range=True):
         self.device = torch.device(device)
         self.reduce_range = reduce_range
+        self.sharded = False   # True: batch-exact across ranks (see _range)
         self.quantized = True
         self.host_io = False
         g = {k: v.detach().cpu().numpy() for k, v in state_dict.items() if torch.is_tensor(v)}
@@ -63,6 +64,20 @@ class DynamicQuantConvNet:
     def _t(self, a):
         return torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
 
+    def _range(self, x):
+        """None (each call uses its own batch range, quantize_dynamic's
+        semantics) unless ``sharded`` is set — this process runs one shard of a
+        batch split over the ranks (qconvnet.dist.sharded_forward): then the
+        range is all-reduced so every shard quantizes exactly as the whole
+        batch would (one 2-float RCCL all-reduce per dynamic Linear; every rank
+        must make the same calls)."""
+        import torch.distributed as dist
+        if not self.sharded or not (dist.is_available() and dist.is_initialized()) \
+                or dist.get_world_size() == 1:
+            return None
+        from qconvnet.dist import global_minmax
+        return global_minmax(ops.minmax_range(x))
+
     @torch.no_grad()
     def __call__(self, x):
         host = not x.is_cuda
@@ -76,12 +91,12 @@ class DynamicQuantConvNet:
                 x = F.max_pool2d(x, 2, 2)
         x = x.reshape(x.shape[0], -1).contiguous()
         w, s, ws, b = self.fc[0]
-        x = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range)
+        x = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range, minmax=self._range(x))
         if self.bn7 is not None:
             x = F.batch_norm(x, self.bn7[0], self.bn7[1], self.bn7[2], self.bn7[3], False, 0.0, 1e-5)
         x = F.relu(x).contiguous()
         w, s, ws, b = self.fc[1]
-        y = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range)
+        y = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range, minmax=self._range(x))
         if host or self.host_io:
             return y.cpu()
         torch.cuda.current_stream(self.device).synchronize()

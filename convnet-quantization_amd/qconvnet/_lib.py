@@ -75,6 +75,8 @@ SIGNATURES = {
     "qcn_avgpool_u8_nhwc": (i32, [vp, i32, i32, i32, f32, i32, f32, i32, vp, vp]),
     "qcn_linear_dynamic_workspace_size": (i64, [i32, i32]),
     "qcn_linear_dynamic_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp]),
+    "qcn_linear_dynamic_range_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp,
+                                           vp]),
     "qcn_linear_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp]),
 }
 

@@ -3,7 +3,9 @@ into contiguous per-rank slices, weights and calibrated qparams replicated
 (calibrated once on rank 0 and broadcast), and ONE exchange per batch: an
 all-gather of the fp32 logits ([shard, 10] per rank) over RCCL/xGMI
 (backend "nccl" is RCCL on ROCm).  The static int8 path is batch-independent,
-so the gathered logits equal a single-GPU run bit for bit.
+so the gathered logits equal a single-GPU run bit for bit.  The dynamic
+(reference-mode) path adds one 2-float all-reduce per dynamic Linear
+(``global_minmax``) so its activation qparams are the whole batch's.
 
 Everything here also runs on CPU with the gloo backend (tests)."""
 from __future__ import annotations
@@ -62,6 +64,19 @@ def gather_logits(local, out=None):
                           device=local.device)
     dist.all_gather_into_tensor(out, local.contiguous())
     return out
+
+
+def global_minmax(mm):
+    """All-reduce a [min, max] pair over the ranks (one 2-float collective:
+    MIN over [min, -max]; negation is exact).  This is the exchange that makes
+    a sharded dynamic-int8 Linear batch-exact: every rank then
+    derives the same ChooseQuantizationParams as a single-GPU run over the
+    whole batch.  Returns a new tensor on mm's device."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return mm
+    t = torch.stack([mm[0], -mm[1]])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return torch.stack([t[0], -t[1]])
 
 
 def sharded_forward(model_fn, x_global, out=None):

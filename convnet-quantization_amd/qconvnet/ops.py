@@ -261,8 +261,21 @@ def classifier(xk, l1, l2, workspace, y1, y2, y2f):
     return True
 
 
-def linear_dynamic(x, w, w_scale, wsum, bias, reduce_range=True, workspace=None, out=None):
-    """quantized::linear_dynamic on the device (fp32 in, fp32 out)."""
+def minmax_range(x, out=None):
+    """[min, max] of a device fp32 tensor as a device float[2] (A2 kernel)."""
+    _need(x, torch.float32, "minmax.x")
+    if out is None:
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+    check(lib().qcn_minmax_reset(_ptr(out), _stream()), "minmax_reset")
+    check(lib().qcn_minmax_f32(_ptr(x), x.numel(), _ptr(out), _stream()), "minmax")
+    return out
+
+
+def linear_dynamic(x, w, w_scale, wsum, bias, reduce_range=True, workspace=None, out=None,
+                   minmax=None):
+    """quantized::linear_dynamic on the device (fp32 in, fp32 out).  With
+    ``minmax`` (device float[2]) the activation qparams come from that range
+    instead of this batch's own (the sharded, batch-exact form)."""
     _need(x, torch.float32, "linear_dynamic.x")
     m, k = x.shape
     n = w.shape[0]
@@ -272,9 +285,16 @@ def linear_dynamic(x, w, w_scale, wsum, bias, reduce_range=True, workspace=None,
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
     per_channel = int(w_scale.numel() > 1)
-    check(lib().qcn_linear_dynamic_f32(_ptr(x), m, k, _ptr(w), n, _ptr(w_scale), per_channel,
-                                       _ptr(wsum), _ptr(bias), int(bool(reduce_range)), _ptr(out),
-                                       _ptr(workspace), _stream()), "linear_dynamic")
+    if minmax is None:
+        check(lib().qcn_linear_dynamic_f32(_ptr(x), m, k, _ptr(w), n, _ptr(w_scale), per_channel,
+                                           _ptr(wsum), _ptr(bias), int(bool(reduce_range)),
+                                           _ptr(out), _ptr(workspace), _stream()), "linear_dynamic")
+    else:
+        _need(minmax, torch.float32, "linear_dynamic.minmax")
+        check(lib().qcn_linear_dynamic_range_f32(_ptr(x), m, k, _ptr(w), n, _ptr(w_scale),
+                                                 per_channel, _ptr(wsum), _ptr(bias),
+                                                 int(bool(reduce_range)), _ptr(minmax), _ptr(out),
+                                                 _ptr(workspace), _stream()), "linear_dynamic_range")
     return out
 
 

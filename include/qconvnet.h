@@ -180,6 +180,15 @@ int qcn_linear_dynamic_f32(const float* x, int m, int k, const int8_t* w, int n,
                            const float* bias, int reduce_range, float* y, void* workspace,
                            void* stream);
 
+/* A8 with the activation range supplied by the caller: minmax points to 2
+ * device floats [min, max] — e.g. the all-reduced range of every rank's shard,
+ * which makes a sharded dynamic Linear batch-exact.  Otherwise
+ * identical to qcn_linear_dynamic_f32. */
+int qcn_linear_dynamic_range_f32(const float* x, int m, int k, const int8_t* w, int n,
+                                 const float* w_scale, int per_channel, const int32_t* wsum,
+                                 const float* bias, int reduce_range, const float* minmax,
+                                 float* y, void* workspace, void* stream);
+
 /* fp32 Linear (fc2 of CustomQuantizedSimpleConvNet stays fp32,
  * custom_quantization_model.py:219): y = x @ w^T + b, with optional ReLU on x
  * (relu_in) applied on load. */

@@ -286,14 +286,17 @@ def quantize_legacy_fma(x, scale, zero_point, qmax=255):
     return np.clip(np.rint(t), 0, qmax).astype(np.uint8)
 
 
-def linear_dynamic(x, qw, s_w, bias, reduce_range=True):
+def linear_dynamic(x, qw, s_w, bias, reduce_range=True, xrange=None):
     """quantized::linear_dynamic (FBGEMM; torch/ao/nn/quantized/dynamic/modules/
     linear.py:50-67): per-call qparams from the batch's min/max
     (ChooseQuantizationParams, qrange [0,127] with reduce_range), LEGACY
     quantize, exact int GEMM, then ReQuantizeForFloat, which the compiled
-    ``requantizeForFloatAvx2`` FMA-contracts: y = fmaf(fp32(acc), fp32(s_x*s_w), b)."""
+    ``requantizeForFloatAvx2`` FMA-contracts: y = fmaf(fp32(acc), fp32(s_x*s_w), b).
+    ``xrange=(min, max)`` overrides the batch range (a shard of a larger batch
+    quantized with the whole batch's range)."""
     x = np.asarray(x, F32)
-    s_x, z_x = choose_qparams_dynamic(x.min(), x.max(), reduce_range=reduce_range)
+    lo, hi = (x.min(), x.max()) if xrange is None else xrange
+    s_x, z_x = choose_qparams_dynamic(lo, hi, reduce_range=reduce_range)
     qx = quantize_legacy_fma(x, s_x, z_x)
     acc = linear_acc(qx, z_x, qw)
     s_w = np.atleast_1d(np.asarray(s_w, F32))

@@ -81,3 +81,62 @@ def test_two_rank_gather_matches_single_process():
         assert not isinstance(res[r], str), res[r]
     assert np.array_equal(res[0], res[1])
     assert np.array_equal(res[0], z["logits"][:8])
+
+
+def _range_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (os.path.join(root, "convnet-quantization_amd"), root, here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from oracle import qref
+        from qconvnet import dist as qd
+        qd.init("gloo")
+        x, qw, s_w, b = _dyn_case()
+        s, e = qd.shard(x.shape[0], world, rank)
+        lo, hi = torch.aminmax(torch.from_numpy(x[s:e]))   # stands in for the device observer
+        mm = qd.global_minmax(torch.stack([lo, hi]))
+        y = qref.linear_dynamic(x[s:e], qw, s_w, b, True, (mm[0].item(), mm[1].item()))
+        q.put((rank, (mm.numpy(), y)))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+
+
+def _dyn_case():
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((16, 256)).astype(np.float32)
+    x[3] *= 6.0          # the batch extremes sit on rank 0's shard only
+    w = (rng.standard_normal((32, 256)) * 0.05).astype(np.float32)
+    from oracle import qref
+    s_w = qref.qparams_symmetric(w.min(), w.max())[0]
+    return x, qref.quantize_weight(w, s_w), s_w, (rng.standard_normal(32) * 0.1).astype(np.float32)
+
+
+def test_sharded_dynamic_linear_is_batch_exact():
+    """§8(f)1: with the 2-float all-reduce of the activation range, the shards
+    of a dynamic-int8 Linear reproduce the whole-batch result exactly (and
+    differ from per-shard ranges, so the exchange is what makes it exact)."""
+    from oracle import qref
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_range_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert not isinstance(res[r], str), res[r]
+    x, qw, s_w, b = _dyn_case()
+    full = qref.linear_dynamic(x, qw, s_w, b, True)
+    assert np.array_equal(res[0][0], np.array([x.min(), x.max()], np.float32))
+    assert np.array_equal(np.concatenate([res[0][1], res[1][1]]), full)
+    per_shard = qref.linear_dynamic(x[8:], qw, s_w, b, True)
+    assert not np.array_equal(per_shard, full[8:])

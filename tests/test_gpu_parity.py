@@ -205,6 +205,27 @@ def test_linear_dynamic_golden(dev, golden_dir):
         assert np.array_equal(got, z[f"d{i}_y"]), f"case {i}: {(got != z[f'd{i}_y']).sum()}"
 
 
+def test_linear_dynamic_shards_with_global_range(dev, golden_dir):
+    """§8(f)1: shards quantized with the whole batch's [min, max] (what the
+    all-reduce of qconvnet.dist.global_minmax supplies) concatenate to the
+    whole-batch golden output; the device observer gives that range."""
+    from qconvnet import ops
+    z = _g(golden_dir, "ops_dynamic_linear.npz")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    for i in range(int(z["n"])):
+        x, w = z[f"d{i}_x"], z[f"d{i}_w"]
+        if x.shape[0] < 2:
+            continue
+        wsum = w.astype(np.int64).sum(1).astype(np.int32)
+        args = (T(w), T(np.atleast_1d(z[f"d{i}_s_w"])), T(wsum), T(z[f"d{i}_b"]))
+        mm = ops.minmax_range(T(x))
+        assert np.array_equal(mm.cpu().numpy(), np.array([x.min(), x.max()], np.float32))
+        h = x.shape[0] // 2
+        parts = [ops.linear_dynamic(T(x[a:b]), *args, minmax=mm).cpu().numpy()
+                 for a, b in ((0, h), (h, x.shape[0]))]
+        assert np.array_equal(np.concatenate(parts), z[f"d{i}_y"]), i
+
+
 @pytest.mark.parametrize("per_channel", [False, True])
 def test_full_net_static_int8_golden(dev, per_channel):
     """Whole static-int8 SimpleConvNet vs torch.ao (fbgemm): logits bit-exact,
