@@ -383,7 +383,9 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
       for (int g = 0; g < C::NG; ++g)
         if (dma && m == (2 * g + 1) * 8 / (2 * C::NG)) {
           __builtin_amdgcn_sched_barrier(0);
+#ifndef QCN_EXP_NODMA
           issue_g(dch, g);
+#endif
         }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -613,7 +615,9 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
       for (int j = 0; j < 4; ++j) {
         const int m = (wp * 4 + j) * 32 + l32;
         const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
-#ifdef QCN_EXP_PAIR_PERM
+#if defined(QCN_EXP_NOEPIA)
+        if (acc[i][j][0] == 0x7fffffff) lds[CB::slot(seg, row + 1, col + 1)] = 1;
+#elif defined(QCN_EXP_PAIR_PERM)
         epilogue_tile_kf<1, true>(&acc[i][j], K, epa, co_base, hi, lds + CB::slot(seg, row + 1, col + 1));
 #else
         epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
