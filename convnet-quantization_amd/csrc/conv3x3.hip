@@ -771,7 +771,11 @@ struct Conv12P {
   static constexpr int OFF_EPI1 = OFF_IN + 2 * IN8;
   static constexpr int OFF_EPI2 = OFF_EPI1 + 12 * 64;
   static constexpr int OFF_CORR2 = OFF_EPI2 + 12 * 64;      // conv2 corr (int32 x 64)
-  static constexpr int LDS = OFF_CORR2 + 4 * 64;
+  // conv1's MFMA A operand, per lane, in the dword-per-tap K order
+  // ([i][lane] v4i), and conv1's corr: built once, read per tile
+  static constexpr int OFF_A1 = OFF_CORR2 + 4 * 64;
+  static constexpr int OFF_CORR1 = OFF_A1 + 2 * 64 * 16;
+  static constexpr int LDS = OFF_CORR1 + 4 * 64;
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
@@ -860,6 +864,30 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
   stage_epik<64, 512>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
   if (tid < 16)
     reinterpret_cast<int4*>(lds + L::OFF_CORR2)[tid] = reinterpret_cast<const int4*>(ep2.corr)[tid];
+  if (tid >= 64 && tid < 80)
+    reinterpret_cast<int4*>(lds + L::OFF_CORR1)[tid - 64] = reinterpret_cast<const int4*>(ep1.corr)[tid - 64];
+  if (wave == 4) {
+    // conv1 A operand in the dword-per-tap K order (k' = 4 tap + c, taps
+    // 0..7) from the [64][32] (k = 3 tap + c) packing
+    const int l32 = lane & 31, hi = lane >> 5;
+    v4i* a1t = reinterpret_cast<v4i*>(lds + L::OFF_A1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint4 r0 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32);
+      const uint4 r1 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32 + 16);
+      const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      auto byte = [&](int k) -> uint32_t { return (wd[k >> 2] >> (8 * (k & 3))) & 0xff; };
+      auto tapw = [&](int t) -> int {   // (w[3t], w[3t+1], w[3t+2], 0)
+        return (int)(byte(3 * t) | (byte(3 * t + 1) << 8) | (byte(3 * t + 2) << 16));
+      };
+      // tap 8's three channels ride in the pad byte (byte 3) of taps 0, 1, 2,
+      // so the whole 27-long K fits one K=32 MFMA step
+      const v4i lo4 = (v4i){tapw(0) | (int)(byte(24) << 24), tapw(1) | (int)(byte(25) << 24),
+                            tapw(2) | (int)(byte(26) << 24), tapw(3)};
+      const v4i hi4 = (v4i){tapw(4), tapw(5), tapw(6), tapw(7)};
+      a1t[i * 64 + lane] = hi ? hi4 : lo4;
+    }
+  }
   const uint32_t padw = xor80(splat_u8(x2_zp));
   const uint4 pad4 = make_uint4(padw, padw, padw, padw);
   for (int e = tid; e < 2 * C::PROWS * 8; e += 512) {
@@ -868,9 +896,14 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
     *reinterpret_cast<uint4*>(lds + buf * L::PATCH + C::slot(0, pr, pc) + chunk * 16) = pad4;
   }
 
-  float xv[12];
-  bool xok[12];
-  // The window index math below depends only on the thread id; laundering it
+  float4 xraw[3];
+  // Window staging, vectorised: producer thread pt < 180 owns window row
+  // rr = pt / 9 and columns 4g-2 .. 4g+1 (g = pt % 9) of all three channels:
+  // three 16-B loads (8-B aligned: dword-aligned is enough) and one 12-byte
+  // [col][c] run in LDS.  Out-of-image rows/columns quantize to in_zp.
+  // stage_load only issues the loads (raw float4s stay in registers, their
+  // latency hidden behind conv1_tile); stage_store selects, quantizes, writes.
+  // The window index math depends only on the thread id; laundering it
   // through an empty asm per use keeps LICM from hoisting ~40 loop-invariant
   // values out of the tile loop (they were spilled: the consumer's MFMA state
   // shares the register budget).
@@ -879,46 +912,45 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
     asm volatile("" : "+v"(v));
     return v;
   };
-  // Window staging, vectorised: producer thread pt < 180 owns window row
-  // rr = pt / 9 and columns 4g-2 .. 4g+1 (g = pt % 9) of all three channels:
-  // three 16-B loads (8-B aligned: dword-aligned is enough) and one 12-byte
-  // [col][c] run in LDS.  Out-of-image rows/columns quantize to in_zp.
+  int xrow_ok = 0;
   auto stage_load = [&](int t) {
     const int n = t >> 1, y0 = (t & 1) * 16;
     const int pt = fresh_ptid();
     const int rr = pt / 9, g = pt % 9;
     const int iy = y0 - 2 + rr, c0 = 4 * g - 2;
     const bool row_ok = pt < 180 && iy >= 0 && iy < 32;
+    xrow_ok = row_ok;
+    // columns c0..c0+3 lie in [0, 32) except for g = 0 (c0 = -2) and g = 8 (c0 = 30):
+    // load from a clamped in-row start, select per element at store time
+    const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
+    // unconditional loads (a clamped, valid row when outside): a divergent
+    // load made the compiler wait for it on the spot
+    const int iyc = iy < 0 ? 0 : (iy > 31 ? 31 : iy);
+    const int nc = n < nimg ? n : nimg - 1;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      // columns c0..c0+3 lie in [0, 32) except for g = 0 (c0 = -2) and g = 8 (c0 = 30):
-      // load from a clamped in-row start and select per element
-      const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
-      const float4 v = row_ok ? *reinterpret_cast<const float4*>(x + (((long)n * 3 + c) * 32 + iy) * 32 + cl)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int col = c0 + e;          // wanted column
-        const int idx = col - cl;        // its position in the loaded 4 (if inside)
-        xv[c * 4 + e] = (idx == 0) ? vv[0] : (idx == 1) ? vv[1] : (idx == 2) ? vv[2] : vv[3];
-        xok[c * 4 + e] = row_ok && col >= 0 && col < 32;
-      }
-    }
+    for (int c = 0; c < 3; ++c)
+      xraw[c] = *reinterpret_cast<const float4*>(x + (((long)nc * 3 + c) * 32 + iyc) * 32 + cl);
   };
   auto stage_store = [&](uint8_t* in8) {  // quantize (aten quantize_per_tensor) -> s8
     const int pt = fresh_ptid();
     if (pt < 180) {
       const int rr = pt / 9, g = pt % 9;
+      const int c0 = 4 * g - 2;
+      const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
       uint32_t wd[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        const int col = c0 + e;          // wanted column
+        const int idx = col - cl;        // its position in the loaded 4 (if inside)
+        const bool ok = xrow_ok && col >= 0 && col < 32;
         uint32_t d = 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
+          const float4 v = xraw[c];
+          const float xv = (idx == 0) ? v.x : (idx == 1) ? v.y : (idx == 2) ? v.z : v.w;
           int q = in_zp;
-          if (xok[c * 4 + e]) {
-            float t = xv[c * 4 + e] * in_inv;
+          if (ok) {
+            float t = xv * in_inv;
             t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
             q = (int)__builtin_rintf(t) + in_zp;
             q = q < 0 ? 0 : (q > 255 ? 255 : q);
@@ -943,40 +975,36 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
     const int y0 = (t & 1) * 16;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
     const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
-    // conv1 A operand in the dword-per-tap K order: step 0 covers taps 0..7
-    // (k' = 4 tap + c, c = 3 -> 0), step 1 tap 8; rebuilt per tile from the
-    // [64][32] (k = 3 tap + c) packing, and the corrected accumulator init
-    // (per tile: keeping them live across the loop would add to the consumer's
-    // register budget)
-    v4i a1[2][2];
+    // conv1 A operand and corrected accumulator init from the LDS tables
+    // (built once in the prologue; LDS latency instead of a dependent L2
+    // round trip at every tile start; re-read per tile so they are not live
+    // across the consumer's MFMA region)
+    v4i a1[2];
     v16i c1[2];
+    {
+      const v4i* a1t = reinterpret_cast<const v4i*>(lds + L::OFF_A1);
+      const int* corr1 = reinterpret_cast<const int*>(lds + L::OFF_CORR1);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint4 r0 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32);
-      const uint4 r1 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32 + 16);
-      const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-      auto byte = [&](int k) -> uint32_t { return (wd[k >> 2] >> (8 * (k & 3))) & 0xff; };
-      auto tapw = [&](int t) -> int {   // (w[3t], w[3t+1], w[3t+2], 0)
-        return (int)(byte(3 * t) | (byte(3 * t + 1) << 8) | (byte(3 * t + 2) << 16));
-      };
-      // constant byte indices (a lane-dependent index would put wd[] in scratch)
-      const v4i lo4 = (v4i){tapw(0), tapw(1), tapw(2), tapw(3)};
-      const v4i hi4 = (v4i){tapw(4), tapw(5), tapw(6), tapw(7)};
-      a1[i][0] = hi ? hi4 : lo4;
-      a1[i][1] = (v4i){hi ? 0 : tapw(8), 0, 0, 0};
-      c1[i] = acc_init_corr(ep1.corr, i * 32, hi);
+      for (int i = 0; i < 2; ++i) {
+        a1[i] = a1t[i * 64 + ln];
+        c1[i] = acc_init_corr(corr1, i * 32, hi);
+      }
     }
     const int* in32 = reinterpret_cast<const int*>(in8);
-    auto bop = [&](int tr, v4i& b0, v4i& b1) {
+    // B operand of one conv1 row: window dwords (c0, c1, c2, 0) per pixel;
+    // low lanes carry taps (0,0) (0,1) (0,2) (1,0) with tap (2,2)'s channel c
+    // in the pad byte of tap (0,c) (v_perm), high lanes (1,1) (1,2) (2,0) (2,1)
+    auto bop = [&](int tr, v4i& b0) {
       const int* r0 = in32 + (tr + 0) * L::IN_C + l32 + 1;   // input cols l32-1 .. l32+1
       const int* r1 = r0 + L::IN_C;
       const int* r2 = r1 + L::IN_C;
-      if (hi == 0) {   // taps (0,0) (0,1) (0,2) (1,0) | (2,2)
-        b0 = (v4i){r0[0], r0[1], r0[2], r1[0]};
-        b1 = (v4i){r2[2], 0, 0, 0};
-      } else {         // taps (1,1) (1,2) (2,0) (2,1)
+      if (hi == 0) {
+        const uint32_t t8 = (uint32_t)r2[2];
+        b0 = (v4i){(int)__builtin_amdgcn_perm((uint32_t)r0[0], t8, 0x00060504u),
+                   (int)__builtin_amdgcn_perm((uint32_t)r0[1], t8, 0x01060504u),
+                   (int)__builtin_amdgcn_perm((uint32_t)r0[2], t8, 0x02060504u), r1[0]};
+      } else {
         b0 = (v4i){r1[1], r1[2], r2[0], r2[1]};
-        b1 = (v4i){0, 0, 0, 0};
       }
     };
     auto rows = [&](auto mode) {
@@ -1009,12 +1037,11 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
             *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
             continue;
           }
-          v4i b0, b1;
-          bop(tr, b0, b1);
+          v4i b0;
+          bop(tr, b0);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc, 0, 0, 0);
+            v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b0, c1[i], 0, 0, 0);
             epilogue_tile_kf<1, true>(&acc, load_epik_lds(ek1, 64, i * 32, hi), ep1, i * 32, hi,
                                       prow_ptr);
           }
@@ -1027,13 +1054,11 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
         const int w = wave - 4;
         const int nr = w < 2 ? 5 : 4;
         auto mfma_row = [&](int tr, v16i (&acc)[2]) {
-          v4i b0, b1;
-          bop(tr, b0, b1);
+          v4i b0;
+          bop(tr, b0);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][0], b0, c1[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i][1], b1, acc[i], 0, 0, 0);
-          }
+          for (int i = 0; i < 2; ++i)
+            acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b0, c1[i], 0, 0, 0);
         };
         v16i acc_n[2];
         mfma_row(w, acc_n);

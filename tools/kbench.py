@@ -26,27 +26,23 @@ from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
-    parts_list = [int(p) for p in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1]
     dev = torch.device("cuda:0")
     fp = torch_ref.reference_fp32_model(0, torch_ref.synthetic_images(64, 1))
     folded = fold_state_dict(fp.state_dict())
     ranges = calibrate(folded, [torch.from_numpy(torch_ref.synthetic_images(64, 1))], "cpu")
     model = QuantizedConvNet(build_qspec(folded, ranges, "static"), dev)
     x = torch.from_numpy(torch_ref.synthetic_images(B, 0)).to(dev)
-    ref = model.run(x).clone()
+    for _ in range(5):
+        model.run(x)
+    torch.cuda.synchronize()
     for rep in range(2):
-        for parts in parts_list:
-            for _ in range(5):
-                out = model.run_split(x, parts)
-            torch.cuda.synchronize()
-            assert torch.equal(out, ref), "split forward differs"
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                model.run_split(x, parts)
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            print(f"batch {B} x {iters} parts {parts}: {dt / iters * 1e3:.3f} ms/forward, "
-                  f"{B * iters / dt / 1e6:.3f} M img/s", flush=True)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            model.run(x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"batch {B} x {iters}: {dt / iters * 1e3:.3f} ms/forward, "
+              f"{B * iters / dt / 1e6:.3f} M img/s", flush=True)
 
 
 if __name__ == "__main__":
