@@ -25,6 +25,7 @@
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
 #include <type_traits>
+#include <cstdlib>
 
 // Diagnostic build only (tools/micro/conv_stamp.hip defines QCN_STAMPS):
 // wave 0 of each workgroup records s_memtime at phase boundaries.
@@ -49,12 +50,17 @@ namespace qcn {
 //   RPAD bytes of padding per staged row,  SPAD per staged image segment
 //   SPLIT store even patch columns before odd ones (pooled layers read stride-2)
 template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
-          int SPAD = 0, bool SPLIT = false>
+          int SPAD = 0, bool SPLIT = false, int WI_ = 2>
 struct ConvCfg {
   static constexpr int kCin = CIN, kCout = COUT;
   static constexpr bool kPool = POOL, kSplit = SPLIT;
   static constexpr int W = HW, H = HW;
-  static constexpr int WCO = COUT / 64;          // waves along cout
+  // wave tile: WI 32-channel blocks (64 or 128 couts) x 128 pixels.  WI = 4
+  // reads 8 fragments per 16 MFMAs instead of 6 per 8 (LDS bytes per MFMA
+  // -33 %) and holds 256 accumulators, so one wave per SIMD
+  static constexpr int WI = WI_;
+  static constexpr int MPS = 4 * WI;             // MFMAs per K-step
+  static constexpr int WCO = COUT / (32 * WI);   // waves along cout
   static constexpr int NWAVES = WCO * WPX;
   static constexpr int NT = NWAVES * 64;         // threads
   static constexpr int PXB = WPX * 128;          // output pixels per workgroup (pre-pool)
@@ -76,7 +82,8 @@ struct ConvCfg {
   static constexpr int OUT = OPX * OS;
   static constexpr int EPI = MAIN > OUT ? MAIN : OUT;  // u | v | mult (fp32 x COUT each)
   static constexpr int LDS = EPI + 12 * COUT;
-  static_assert(CIN % 64 == 0 && COUT % 64 == 0, "channel multiples of 64");
+  static_assert(CIN % 64 == 0 && COUT % (32 * WI) == 0, "channel multiples");
+  static_assert(WI == 2 || WI == 4, "wave tile of 64 or 128 couts");
   static_assert(PSP % 16 == 0 && RPAD % 16 == 0 && SPAD % 16 == 0, "16-B aligned layout");
   static_assert(PXB % W == 0, "workgroup covers whole rows");
   static_assert(PXB >= IMG ? (PXB % IMG == 0) : (H % R == 0), "rows tile the image");
@@ -316,8 +323,10 @@ struct PatchAddr {
 // (ch-1,1)), so the DMA of ch+2 into that buffer is issued during that step.
 template <class C>
 QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* __restrict__ wpk,
-                           const int* __restrict__ corr, int wave, int lane, v16i (&acc)[2][4]) {
+                           const int* __restrict__ corr, int wave, int lane,
+                           v16i (&acc)[C::WI][4]) {
   constexpr int CB = C::kCin / 64;
+  constexpr int WI = C::WI, MPS = C::MPS;
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
   // weight ring: K-chunk ch (64 input channels of one tap, all COUT rows
@@ -334,12 +343,12 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
     glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
   };
   const PatchAddr<C> pa(wp, l32, hi);
-  // A operand: row wc*64 + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
-  const int arow = wc * 64 + l32;
-  const int aswz = (arow >> 2) & 3;  // same for arow + 32
+  // A operand: row wc*32*WI + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
+  const int arow = wc * 32 * WI + l32;
+  const int aswz = (arow >> 2) & 3;  // same for arow + 32i
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const v16i c0 = acc_init_corr(corr, wc * 64 + i * 32, hi);
+  for (int i = 0; i < WI; ++i) {
+    const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = c0;
   }
@@ -366,22 +375,22 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
     return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 +
                                          kk * 32);
   };
-  // one step: 8 MFMAs on (fa, fb); reads of step (rch, rkk) into (fan, fbn)
-  // interleaved; DMA pieces of chunk dch spread over the MFMAs
-  auto step = [&](v4i (&fan)[2], v4i (&fbn)[4], int rch, int rkk, bool rd,
-                  const v4i (&fa)[2], const v4i (&fb)[4], bool dma, int dch) {
+  // one step: MPS MFMAs on (fa, fb); reads of step (rch, rkk) into (fan, fbn)
+  // interleaved one per MFMA; DMA pieces of chunk dch spread over the MFMAs
+  auto step = [&](v4i (&fan)[WI], v4i (&fbn)[4], int rch, int rkk, bool rd,
+                  const v4i (&fa)[WI], const v4i (&fb)[4], bool dma, int dch) {
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
+    for (int m = 0; m < MPS; ++m) {
       if (rd) {
-        if (m < 2) fan[m] = rd_a(rch, rkk, m);
-        else if (m < 6) fbn[m - 2] = rd_b(rch, rkk, m - 2);
+        if (m < WI) fan[m] = rd_a(rch, rkk, m);
+        else if (m < WI + 4) fbn[m - WI] = rd_b(rch, rkk, m - WI);
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[m >> 2][m & 3] =
-          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m >> 2], fb[m & 3], acc[m >> 2][m & 3], 0, 0, 0);
+      acc[m / 4][m % 4] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / 4], fb[m % 4], acc[m / 4][m % 4], 0, 0, 0);
 #pragma unroll
       for (int g = 0; g < C::NG; ++g)
-        if (dma && m == (2 * g + 1) * 8 / (2 * C::NG)) {
+        if (dma && m == (2 * g + 1) * MPS / (2 * C::NG)) {
           __builtin_amdgcn_sched_barrier(0);
 #ifndef QCN_EXP_NODMA
           issue_g(dch, g);
@@ -390,9 +399,9 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  v4i fa0[2], fb0[4], fa1[2], fb1[4];
-  fa0[0] = rd_a(0, 0, 0);
-  fa0[1] = rd_a(0, 0, 1);
+  v4i fa0[WI], fb0[4], fa1[WI], fb1[4];
+#pragma unroll
+  for (int i = 0; i < WI; ++i) fa0[i] = rd_a(0, 0, i);
 #pragma unroll
   for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
 #pragma unroll
@@ -418,7 +427,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 // Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
 // the workgroup's contiguous NHWC output span with 16-B stores.
 template <class C>
-QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, int nimg,
+QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* lds, int nimg,
                            int wave, int lane, int tid, uint8_t* __restrict__ y,
                            const float* ek_override = nullptr) {
   const int wc = wave % C::WCO, wp = wave / C::WCO;
@@ -428,8 +437,8 @@ QCN_DEV void conv_epilogue(v16i (&acc)[2][4], const ConvEpi& ep, uint8_t* lds, i
   uint8_t* lout = lds;  // the patch / weight ring is dead after the last barrier
   const float* ek = ek_override ? ek_override : reinterpret_cast<const float*>(lds + C::EPI);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int co_base = wc * 64 + i * 32;
+  for (int i = 0; i < C::WI; ++i) {
+    const int co_base = wc * 32 * C::WI + i * 32;
     const EpiK K = load_epik_lds(ek, COUT, co_base, hi);
     if constexpr (POOL) {
       const int opx = wp * 32 + l32;
@@ -516,6 +525,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                          const int8_t* __restrict__ wpk, ConvEpi ep,
                          uint8_t* __restrict__ y) {
   using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  static_assert(C::NT == COUT * WPX, "64-cout wave tiles");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* patch = lds;
 
@@ -533,7 +543,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 
   QCN_STAMP(1);
   QCN_STAMP(2);
-  v16i acc[2][4];
+  v16i acc[C::WI][4];
   conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
   QCN_STAMP(3);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
@@ -551,7 +561,7 @@ template <class CA, class CB>
 struct PairCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
-                CA::W == CB::W, "same whole-image tiling");
+                CA::W == CB::W && CA::WI == CB::WI, "same whole-image tiling");
   static constexpr int MAIN_A = CA::PATCH + 3 * CA::WBUF;
   static constexpr int MAIN_B = CB::PATCH + 3 * CB::WBUF;
   static constexpr int MAIN = MAIN_A > MAIN_B ? MAIN_A : MAIN_B;
@@ -567,7 +577,7 @@ struct PairCfg {
 };
 
 template <class CA, class CB>
-__global__ __launch_bounds__(CA::NT, 2)
+__global__ __launch_bounds__(CA::NT, CA::WI == 4 ? 1 : 2)
 void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                      const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                      const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
@@ -585,7 +595,7 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
   QCN_STAMP(1);
 
-  v16i acc[2][4];
+  v16i acc[CA::WI][4];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
   QCN_STAMP(2);
 
@@ -608,8 +618,8 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
     const int wc = wave % CA::WCO, wp = wave / CA::WCO;
     const int l32 = lane & 31, hi = lane >> 5;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co_base = wc * 64 + i * 32;
+    for (int i = 0; i < CA::WI; ++i) {
+      const int co_base = wc * 32 * CA::WI + i * 32;
       const EpiK K = load_epik_lds(eka, CA::kCout, co_base, hi);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1404,14 +1414,32 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   }
   hipStream_t st = (hipStream_t)stream;
   using namespace qcn;
-  if (hw == 16 && cin == 64 && cmid == 128 && cout == 128)
+  // wave tile: 64 couts x 128 pixels, two waves per SIMD (two workgroups per
+  // CU for conv3+conv4); QCN_PAIR_WI=4 selects 128 x 128 tiles at one wave
+  // per SIMD (a third fewer LDS bytes per MFMA, but no partner wave to cover
+  // the epilogues: measured 63 vs 53 us and 56 vs 51 us)
+  static const int wi = [] {
+    const char* e = getenv("QCN_PAIR_WI");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
+    if (wi == 4)
+      return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 4>,
+                         ConvCfg<128, 128, 16, true, 4, 16, 32, 0, true, 4>>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                        ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256)
+  }
+  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
+    if (wi == 4)
+      return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false, 4>,
+                         ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true, 4>>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
                        ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+  }
   return QCN_ERR_UNSUPPORTED;
 }
 
