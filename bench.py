@@ -45,6 +45,7 @@ MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
 MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
 MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
 MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
+MAC_PER_IMAGE["net"] = sum(MAC_PER_IMAGE[f"conv{i}"] for i in range(1, 7))
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -56,7 +57,8 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "conv12": 3 * 32 * 32 * 4 + 16 * 16 * 64,
                  "fc12": 4096 + 512 + 10 + 40,
                  "conv34": 16 * 16 * 64 + 8 * 8 * 128,
-                 "conv56": 8 * 8 * 128 + 4 * 4 * 256}
+                 "conv56": 8 * 8 * 128 + 4 * 4 * 256,
+                 "net": 3 * 32 * 32 * 4 + 4 * 4 * 256}
 HBM_BOUND = {"conv1"}
 
 

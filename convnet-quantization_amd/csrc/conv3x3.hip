@@ -398,6 +398,15 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
         }
       __builtin_amdgcn_sched_barrier(0);
     }
+    // pin the step's MFMAs here: they are side-effect free, and IR sinking
+    // could otherwise move them past the next barrier towards the epilogue
+    // (the fragment registers then stay live, and spill, across the loop)
+    if constexpr (WI == 2) {   // (WI = 4 keeps its accumulators in AGPRs)
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]));
+    }
   };
   v4i fa0[WI], fb0[4], fa1[WI], fb1[4];
 #pragma unroll
@@ -428,7 +437,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 // the workgroup's contiguous NHWC output span with 16-B stores.
 template <class C>
 QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* lds, int nimg,
-                           int wave, int lane, int tid, uint8_t* __restrict__ y,
+                           int wave, int lane, int tid, uint8_t* __restrict__ y, int tile,
                            const float* ek_override = nullptr) {
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
@@ -452,7 +461,7 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
     }
   }
   __syncthreads();
-  const long out0 = (long)blockIdx.x * C::OPX;
+  const long out0 = (long)tile * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
   if (ep.kmajor) {
     // chunk-major for the classifier GEMM: 32-byte chunk kc of image n at
@@ -481,7 +490,7 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
 // unconditional batches (halo / tail lanes read a valid dummy address and are
 // replaced afterwards) so a thread keeps BATCH 16-B loads in flight instead of
 // one dependent HBM round trip per element.
-template <class C>
+template <class C, bool BYPASS_L1 = false>
 QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int n0, int y0,
                          uint8_t* patch, int tid) {
   constexpr int CIN = C::kCin;
@@ -507,7 +516,12 @@ QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int 
       inside[k] = n < nimg && yy >= 0 && yy < C::H && xx >= 0 && xx < C::W;
       dst[k] = (it < TOTAL && b0 + k < NITER) ? C::slot(seg, pr, pc) + chunk * 16 : -1;
       const long src = inside[k] ? (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16 : 0;
-      v[k] = *reinterpret_cast<const uint4*>(x + src);
+      if constexpr (BYPASS_L1) {   // nt: served by L2, never a stale L1 line
+        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(x + src));
+        v[k] = make_uint4((uint32_t)t[0], (uint32_t)t[1], (uint32_t)t[2], (uint32_t)t[3]);
+      } else {
+        v[k] = *reinterpret_cast<const uint4*>(x + src);
+      }
     }
 #pragma unroll
     for (int k = 0; k < BATCH; ++k) {
@@ -546,7 +560,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   v16i acc[C::WI][4];
   conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
   QCN_STAMP(3);
-  conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y);
+  conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y, (int)blockIdx.x);
   QCN_STAMP(5);
 }
 
@@ -576,15 +590,15 @@ struct PairCfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <class CA, class CB>
-__global__ __launch_bounds__(CA::NT, CA::WI == 4 ? 1 : 2)
-void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                     const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
-                     const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+template <class CA, class CB, bool BYPASS_L1 = false>
+QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                           const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                           const int8_t* __restrict__ wb, ConvEpi epb,
+                           uint8_t* __restrict__ y) {
   using P = PairCfg<CA, CB>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long p0 = (long)blockIdx.x * CA::PXB;
+  const long p0 = (long)tile * CA::PXB;
   const int n0 = (int)(p0 / CA::IMG);
   const int y0 = (int)((p0 % CA::IMG) / CA::W);
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
@@ -592,7 +606,7 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   QCN_STAMP(0);
   stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
-  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
+  stage_patch<CA, BYPASS_L1>(x, nimg, x_zp, n0, y0, lds, tid);
   QCN_STAMP(1);
 
   v16i acc[CA::WI][4];
@@ -640,8 +654,16 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   QCN_STAMP(3);
   conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
   QCN_STAMP(4);
-  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, ekb);
+  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
   QCN_STAMP(5);
+}
+
+template <class CA, class CB>
+__global__ __launch_bounds__(CA::NT, CA::WI == 4 ? 1 : 2)
+void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                     const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                     const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  convpair_body<CA, CB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
 // --------------------------------------------------------------------------
@@ -843,19 +865,19 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
   }
 }
 
-__global__ __launch_bounds__(512, 1)
-void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
-                    const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
-                    const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
+// Tiles t0, t0 + ts, ..., (T of them; tile = half image) through the
+// producer/consumer pipeline.  512 threads, LDS layout Conv12P.
+QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, int nimg,
+                          float in_inv, int in_zp, const int8_t* __restrict__ w1, ConvEpi ep1,
+                          int x2_zp, const int8_t* __restrict__ w2, ConvEpi ep2,
+                          uint8_t* __restrict__ y) {
   using C = Conv2Cfg;
   using L = Conv12P;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool producer = wave >= 4;
   const int ptid = tid - 256;
-  const int ntiles = 2 * nimg;
-  const int T = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  auto tile_of = [&](int j) { return (int)blockIdx.x + j * (int)gridDim.x; };
+  auto tile_of = [&](int j) { return t0 + j * ts; };
   uint8_t* patch0 = lds;
   uint8_t* patch1 = lds + L::PATCH;
   uint8_t* in8_0 = lds + L::OFF_IN;
@@ -1222,6 +1244,65 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
 #endif
 }
 
+__global__ __launch_bounds__(512, 1)
+void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
+                    const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
+                    const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
+  const int ntiles = 2 * nimg;
+  const int T = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  conv12p_body((int)blockIdx.x, (int)gridDim.x, T, x, nimg, in_inv, in_zp, w1, ep1, x2_zp, w2, ep2, y);
+}
+
+// --------------------------------------------------------------------------
+// The whole conv stack of the static int8 SimpleConvNet in one launch: each
+// workgroup (one per CU, LDS-bound) takes a group of 4 images through
+// conv1+conv2 (8 half-image tiles, producer/consumer pipeline), conv3+conv4
+// (two 2-image tiles, 8 waves) and conv5+conv6 (one 4-image tile), writing
+// a2 / a4 to HBM and re-reading them itself (L2-hot, same XCD, nt loads past
+// the L1).  Images are independent, so no workgroup ever waits for another:
+// no kernel boundaries (their tails and the all-CU HBM bursts of each
+// prologue), no launch gaps.
+using NetC3 = ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false>;
+using NetC4 = ConvCfg<128, 128, 16, true, 4, 16, 32, 0, true>;
+using NetC5 = ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>;
+using NetC6 = ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>;
+
+struct NetArgs {
+  const float* x; int nimg; float in_inv; int in_zp;
+  const int8_t* w1; ConvEpi ep1; int x2_zp; const int8_t* w2; ConvEpi ep2;
+  uint8_t* a2;
+  const int8_t* w3; ConvEpi ep3; int x3_zp; int x4_zp; const int8_t* w4; ConvEpi ep4;
+  uint8_t* a4;
+  const int8_t* w5; ConvEpi ep5; int x5_zp; int x6_zp; const int8_t* w6; ConvEpi ep6;
+  uint8_t* y;
+  int phases;   // diagnostic: bit 0 conv1+2, bit 1 conv3+4, bit 2 conv5+6 (QCN_NET_PHASES; 7 = all)
+};
+
+constexpr int net_lds_bytes() {
+  constexpr int a = Conv12P::LDS, b = PairCfg<NetC3, NetC4>::LDS, c = PairCfg<NetC5, NetC6>::LDS;
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
+__global__ __launch_bounds__(512, 1)
+void net_kernel(NetArgs a) {
+  static_assert(NetC3::NT == 512 && NetC5::NT == 512, "8-wave tiles");
+  const int g = (int)blockIdx.x;   // one group of 4 images per workgroup
+  if (a.phases & 1)
+    conv12p_body(8 * g, 1, 8, a.x, a.nimg, a.in_inv, a.in_zp, a.w1, a.ep1, a.x2_zp, a.w2, a.ep2, a.a2);
+  // this workgroup's a2 stores have reached L2 before any wave re-reads them
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < ((a.phases & 2) ? 2 : 0); ++t) {
+    convpair_body<NetC3, NetC4, true>(2 * g + t, a.a2, a.nimg, a.x3_zp, a.w3, a.ep3, a.x4_zp, a.w4,
+                                      a.ep4, a.a4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (a.phases & 4)
+    convpair_body<NetC5, NetC6, true>(g, a.a4, a.nimg, a.x5_zp, a.w5, a.ep5, a.x6_zp, a.w6, a.ep6, a.y);
+}
+
 // --------------------------------------------------------------------------
 // Generic fallback (any CIN/COUT/H/W, no MFMA): one thread per output element.
 // Used only for shapes without a tuned instantiation (unit tests, odd sizes).
@@ -1415,27 +1496,15 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   hipStream_t st = (hipStream_t)stream;
   using namespace qcn;
   // wave tile: 64 couts x 128 pixels, two waves per SIMD (two workgroups per
-  // CU for conv3+conv4); QCN_PAIR_WI=4 selects 128 x 128 tiles at one wave
-  // per SIMD (a third fewer LDS bytes per MFMA, but no partner wave to cover
-  // the epilogues: measured 63 vs 53 us and 56 vs 51 us)
-  static const int wi = [] {
-    const char* e = getenv("QCN_PAIR_WI");
-    return e && atoi(e) == 4 ? 4 : 2;
-  }();
+  // CU for conv3+conv4).  ConvCfg's WI = 4 (128 x 128 tiles, one wave per
+  // SIMD, a third fewer LDS bytes per MFMA) measured slower with no partner
+  // wave to cover the epilogues (63 vs 53 us, 56 vs 51 us) and is not built.
   if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
-    if (wi == 4)
-      return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 4>,
-                         ConvCfg<128, 128, 16, true, 4, 16, 32, 0, true, 4>>(
-          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                        ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
-    if (wi == 4)
-      return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false, 4>,
-                         ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true, 4>>(
-          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
                        ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
@@ -1514,6 +1583,42 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   hipLaunchKernelGGL(qcn::conv12p_kernel, dim3(grid), dim3(512), qcn::Conv12P::LDS,
                      (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
                      w2_packed, ep2, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_convnet_static_u8(const float* x, int nimg, float in_scale, int in_zp,
+                          const qcn_conv_layer_t* layers, int kmajor, uint8_t* a2, uint8_t* a4,
+                          uint8_t* y, void* stream) {
+  if (!x || !layers || !a2 || !a4 || !y) return QCN_ERR_ARG;
+  if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
+  for (int i = 0; i < 6; ++i) {
+    const qcn_conv_layer_t& l = layers[i];
+    if (!l.w_packed || !l.u || !l.v || !l.mult || !l.corr) return QCN_ERR_ARG;
+    if (l.x_zp < 0 || l.x_zp > 255 || l.y_zp < 0 || l.y_zp > 255) return QCN_ERR_ARG;
+  }
+  if (nimg % 4 != 0) return QCN_ERR_UNSUPPORTED;   // groups of 4 images per workgroup
+  auto epi = [](const qcn_conv_layer_t& l, int km) {
+    return qcn::ConvEpi{l.u, l.v, l.mult, l.corr, l.y_zp, l.relu ? l.y_zp : 0, 0, 0.f, 0, 0.f, 0, km};
+  };
+  const qcn_conv_layer_t* L = layers;
+  qcn::NetArgs a{x, nimg, 1.0f / in_scale, in_zp,
+                 L[0].w_packed, epi(L[0], 0), L[1].x_zp, L[1].w_packed, epi(L[1], 0), a2,
+                 L[2].w_packed, epi(L[2], 0), L[2].x_zp, L[3].x_zp, L[3].w_packed, epi(L[3], 0), a4,
+                 L[4].w_packed, epi(L[4], 0), L[4].x_zp, L[5].x_zp, L[5].w_packed,
+                 epi(L[5], kmajor ? 1 : 0), y, 7};
+  static const int phases = [] {
+    const char* e = getenv("QCN_NET_PHASES");
+    return e ? atoi(e) : 7;
+  }();
+  a.phases = phases;
+  static bool attr_done = false;
+  if (!attr_done) {
+    if (hipFuncSetAttribute((const void*)qcn::net_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            qcn::net_lds_bytes()) != hipSuccess)
+      return QCN_ERR_HIP;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL(qcn::net_kernel, dim3(nimg / 4), dim3(512), qcn::net_lds_bytes(), (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
