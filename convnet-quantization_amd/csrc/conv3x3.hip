@@ -183,6 +183,7 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
       if constexpr (NQ == 4) a[e] = max(max(a[e], accs[1][rg]), max(accs[2][rg], accs[3][rg]));
     }
     if constexpr (FAST) {
+#ifdef QCN_PK_REQ
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
         const int rg = 4 * g + e;
@@ -193,6 +194,18 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
         wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.x, e, wd);
         wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
       }
+#else
+      // scalar fma / mul, kept scalar (the SLP vectorizer would re-pack them):
+      // packed fp32 issues slower beside a partner wave's MFMAs
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rg = 4 * g + e;
+        float f = __builtin_fmaf(K.u[rg], K.v[rg], (float)a[e]);
+        f = f * K.m[rg];
+        asm volatile("" : "+v"(f));
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
+      }
+#endif
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -1101,6 +1114,21 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           // requant both 32-channel halves in stages (independent pairs
           // interleave instead of a dependent fma -> mul -> cvt chain per pair)
           v2f t[2][8];
+#ifndef QCN_PK_REQ
+          // scalar fma / mul: packed fp32 beside another wave's MFMAs costs more
+          // issue than two scalar ops (MI355X_MICROARCH 'price of one filler');
+          // measured 53.5 -> 45.4 us for this kernel (tools/micro/flag_ab.sh)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              float f = (float)acc[i][e];
+              f = __builtin_fmaf(u[i][e], sv, f);
+              f = f * (MODE == 1 ? sm : m[i][e]);
+              asm volatile("" : "+v"(f));   // keep the SLP vectorizer from re-packing
+              t[i][e >> 1][e & 1] = f;
+            }
+#else
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1117,6 +1145,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #pragma unroll
             for (int pr = 0; pr < 8; ++pr)
               t[i][pr] = t[i][pr] * (MODE == 1 ? (v2f){sm, sm} : (v2f){m[i][2 * pr], m[i][2 * pr + 1]});
+#endif
           uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
           // the lane's 4-channel groups 8g + 4hi go straight to their dwords in
           // the patch row (v_permlane32_swap costs ~25 cycles each,
