@@ -25,6 +25,22 @@
 
 namespace qcn {
 
+// fp32(fp32(acc) + u*v) * mult for two channels (FBGEMM requant before the
+// rounding).  Scalar fma / mul kept scalar: packed fp32 issues slower beside a
+// partner wave's MFMAs (QCN_PK_REQ builds the packed form for A/B).
+QCN_DEV v2f requant2(int a0, int a1, v2f u, v2f v, v2f m) {
+#ifdef QCN_PK_REQ
+  return __builtin_elementwise_fma(u, v, (v2f){(float)a0, (float)a1}) * m;
+#else
+  float x = __builtin_fmaf(u.x, v.x, (float)a0), y = __builtin_fmaf(u.y, v.y, (float)a1);
+  x = x * m.x;
+  y = y * m.y;
+  asm volatile("" : "+v"(x), "+v"(y));
+  return (v2f){x, y};
+#endif
+}
+
+
 struct ZpLines {
   uint8_t b[256][32];
 };
@@ -244,8 +260,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int h2 = 2 * g + h;
-            const v2f af = {(float)acc[i][j][2 * h2], (float)acc[i][j][2 * h2 + 1]};
-            const v2f ab = __builtin_elementwise_fma(u[h2], v[h2], af) * mu[h2];
+            const v2f ab = requant2(acc[i][j][2 * h2], acc[i][j][2 * h2 + 1], u[h2], v[h2], mu[h2]);
             d[h] = (v2f){__builtin_amdgcn_fmed3f(__builtin_rintf(ab.x), nz3.x, hz3.x),
                          __builtin_amdgcn_fmed3f(__builtin_rintf(ab.y), nz3.x, hz3.x)} * s3;
           }
@@ -301,8 +316,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   }
 
   // Epilogue phase 1 (accumulator layout: lane (l32, hi) of tile (i, j) holds
-  // pixel l32, channels 8g + 4hi + e): FBGEMM requant to u8 — fma / mul as
-  // packed fp32 pairs, v_cvt_pk_u8_f32 (RNE + saturate) standing in for
+  // pixel l32, channels 8g + 4hi + e): FBGEMM requant to u8 — scalar fma / mul
+  // (requant2), v_cvt_pk_u8_f32 (RNE + saturate) standing in for
   // rint/+zp/clamp when zp == 0 — and dword writes into the LDS tile
   // [BM][OS] (no lane transposes).
   const bool fast = a.zp_y == 0;
@@ -326,8 +341,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
       v2f ab[8];
 #pragma unroll
       for (int h2 = 0; h2 < 8; ++h2) {
-        const v2f af = {(float)acc[i][j][2 * h2], (float)acc[i][j][2 * h2 + 1]};
-        ab[h2] = __builtin_elementwise_fma(u[h2], v[h2], af) * mu[h2];
+        ab[h2] = requant2(acc[i][j][2 * h2], acc[i][j][2 * h2 + 1], u[h2], v[h2], mu[h2]);
       }
       uint32_t* od = reinterpret_cast<uint32_t*>(lds + ((wm * C::JT + j) * 32 + l32) * C::OS + cl) + hi;
       if (fast) {
