@@ -42,6 +42,10 @@ __device__ unsigned long long qcn_stamps[1 << 16][8];
 #define QCN_STAMP(k) do {} while (0)
 #endif
 
+#ifndef QCN_PROD_PRIO
+#define QCN_PROD_PRIO 2   // conv12 producer waves' issue priority
+#endif
+
 namespace qcn {
 
 // Patch layout knobs (chosen per layer by an offline bank-conflict search so
@@ -1016,7 +1020,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb) {
     // producer waves issue first: their VALU-bound conv1 is the longer phase,
     // the consumer's MFMAs fill the gaps (measured 53.6 vs 59.2 us)
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(QCN_PROD_PRIO);
     const int y0 = (t & 1) * 16;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
     const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
