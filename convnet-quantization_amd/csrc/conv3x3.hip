@@ -199,14 +199,13 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
         wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
       }
 #else
-      // scalar fma / mul, kept scalar (the SLP vectorizer would re-pack them):
+      // scalar fma / mul (built with -fno-slp-vectorize so they stay scalar):
       // packed fp32 issues slower beside a partner wave's MFMAs
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rg = 4 * g + e;
         float f = __builtin_fmaf(K.u[rg], K.v[rg], (float)a[e]);
         f = f * K.m[rg];
-        asm volatile("" : "+v"(f));
         wd = __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
       }
 #endif
@@ -1119,9 +1118,10 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           // interleave instead of a dependent fma -> mul -> cvt chain per pair)
           v2f t[2][8];
 #ifndef QCN_PK_REQ
-          // scalar fma / mul: packed fp32 beside another wave's MFMAs costs more
-          // issue than two scalar ops (MI355X_MICROARCH 'price of one filler');
-          // measured 53.5 -> 45.4 us for this kernel (tools/micro/flag_ab.sh)
+          // scalar fma / mul (-fno-slp-vectorize keeps them scalar): packed fp32
+          // beside another wave's MFMAs costs more issue than two scalar ops
+          // (MI355X_MICROARCH 'price of one filler'); 53.5 -> 45.4 us here
+          // (tools/micro/flag_ab.sh)
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1129,7 +1129,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
               float f = (float)acc[i][e];
               f = __builtin_fmaf(u[i][e], sv, f);
               f = f * (MODE == 1 ? sm : m[i][e]);
-              asm volatile("" : "+v"(f));   // keep the SLP vectorizer from re-packing
               t[i][e >> 1][e & 1] = f;
             }
 #else

@@ -26,8 +26,9 @@
 namespace qcn {
 
 // fp32(fp32(acc) + u*v) * mult for two channels (FBGEMM requant before the
-// rounding).  Scalar fma / mul kept scalar: packed fp32 issues slower beside a
-// partner wave's MFMAs (QCN_PK_REQ builds the packed form for A/B).
+// rounding).  Scalar fma / mul (the build's -fno-slp-vectorize keeps them
+// scalar): packed fp32 issues slower beside a partner wave's MFMAs
+// (QCN_PK_REQ builds the packed form for A/B).
 QCN_DEV v2f requant2(int a0, int a1, v2f u, v2f v, v2f m) {
 #ifdef QCN_PK_REQ
   return __builtin_elementwise_fma(u, v, (v2f){(float)a0, (float)a1}) * m;
@@ -35,7 +36,6 @@ QCN_DEV v2f requant2(int a0, int a1, v2f u, v2f v, v2f m) {
   float x = __builtin_fmaf(u.x, v.x, (float)a0), y = __builtin_fmaf(u.y, v.y, (float)a1);
   x = x * m.x;
   y = y * m.y;
-  asm volatile("" : "+v"(x), "+v"(y));
   return (v2f){x, y};
 #endif
 }

@@ -8,7 +8,7 @@ mkdir -p $B/convnet-quantization_amd/csrc $B/tools/micro
 cp convnet-quantization_amd/csrc/*.hpp $B/convnet-quantization_amd/csrc/
 cp tools/ab/conv3x3_base.hip $B/convnet-quantization_amd/csrc/conv3x3.hip
 cp tools/micro/conv_stamp.hip $B/tools/micro/
-F="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -DQCN_STAMPS -Iinclude"
+F="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -DQCN_STAMPS -Iinclude"
 hipcc $F -I$B/convnet-quantization_amd/csrc $B/tools/micro/conv_stamp.hip -o /tmp/stamp_base
 hipcc $F -Iconvnet-quantization_amd/csrc tools/micro/conv_stamp.hip -o /tmp/stamp_new
 for i in $(seq $N); do

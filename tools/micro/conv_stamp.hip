@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
@@ -151,6 +152,11 @@ static void runpair(int cin, int cmid, int cout, int hw, int nimg) {
 }
 
 int main() {
+  if (const char* e = getenv("QCN_SWEEP12")) {   // conv12 launch time vs batch
+    (void)e;
+    for (int nb : {256, 512, 1024, 2048, 4096, 8192}) run12(nb);
+    return 0;
+  }
   const int n = 1024;
   runpair(64, 128, 128, 16, n);
   runpair(128, 256, 256, 8, n);

@@ -2,7 +2,7 @@
 # usage (on the box, from the repo root): bash tools/micro/flag_ab.sh "-DFLAG" [reps]
 set -e
 FL=$1; N=${2:-2}
-F="--offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -DQCN_STAMPS -Iinclude -Iconvnet-quantization_amd/csrc"
+F="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -std=c++17 -DQCN_STAMPS -Iinclude -Iconvnet-quantization_amd/csrc"
 hipcc $F tools/micro/conv_stamp.hip -o /tmp/stamp_a
 hipcc $F $FL tools/micro/conv_stamp.hip -o /tmp/stamp_b
 for i in $(seq $N); do
