@@ -1108,14 +1108,9 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           for (int i = 0; i < 2; ++i)
             acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b0, c1[i], 0, 0, 0);
         };
-        v16i acc_n[2];
-        mfma_row(w, acc_n);
-        for (int kr = 0; kr < nr; ++kr) {
-          const int tr = w + 4 * kr;
-          v16i acc[2] = {acc_n[0], acc_n[1]};
-          if (kr + 1 < nr) mfma_row(tr + 4, acc_n);
-          // requant both 32-channel halves in stages (independent pairs
-          // interleave instead of a dependent fma -> mul -> cvt chain per pair)
+        // requantize one conv1 row (both 32-channel halves) straight into its
+        // conv2 patch row
+        auto requant_row = [&](const v16i (&acc)[2], int tr) {
           v2f t[2][8];
 #ifndef QCN_PK_REQ
           // scalar fma / mul (-fno-slp-vectorize keeps them scalar): packed fp32
@@ -1168,6 +1163,21 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
             *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
             *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
+          }
+        };
+        // two named accumulator sets in ping-pong (a copy per row cost 16
+        // v_mov_b64): row kr+1's im2col reads and MFMAs go out before row kr's
+        // requant, so the VALU never waits on an MFMA result
+        v16i acc_x[2], acc_y[2];
+        mfma_row(w, acc_x);
+#pragma unroll
+        for (int kr = 0; kr < 5; kr += 2) {
+          if (kr >= nr) break;
+          if (kr + 1 < nr) mfma_row(w + 4 * (kr + 1), acc_y);
+          requant_row(acc_x, w + 4 * kr);
+          if (kr + 1 < nr) {
+            if (kr + 2 < nr) mfma_row(w + 4 * (kr + 2), acc_x);
+            requant_row(acc_y, w + 4 * (kr + 1));
           }
         }
       }
