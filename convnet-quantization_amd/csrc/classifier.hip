@@ -140,25 +140,39 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(const int* __restrict__ 
   *reinterpret_cast<uint2*>(y1 + (long)row * FC_N1 + f0) = make_uint2(lo, hw);
 
   // fc2: exact sum_k (q1 - z1) * w2[o][k] over this lane's 8 k, for all
-  // outputs at once, then the wave reductions interleaved (independent chains)
+  // outputs at once: (q1 - z1) w = s8(q1 ^ 0x80) w + (128 - z1) w, so two
+  // v_dot4_i32_i8 on the xor'd fc1 bytes plus (128 - z1) * sum(w) (two more
+  // dot4 against 0x01010101) — no 32-bit multiplies
+  const int ql = (int)(lo ^ 0x80808080u), qh = (int)(hw ^ 0x80808080u);
+  const int zc = 128 - hd.z1;
   int sacc[FC_N2];
 #pragma unroll
   for (int o = 0; o < FC_N2; ++o) {
-    sacc[o] = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int wb = (int)(int8_t)(((e < 4 ? wv[o].x : wv[o].y) >> (8 * (e & 3))) & 0xff);
-      sacc[o] += (q[e] - hd.z1) * wb;
-    }
+    const int wx = (int)wv[o].x, wy = (int)wv[o].y;
+    const int ws = __builtin_amdgcn_sdot4(wx, 0x01010101, __builtin_amdgcn_sdot4(wy, 0x01010101, 0, false), false);
+    sacc[o] = __builtin_amdgcn_sdot4(ql, wx, __builtin_amdgcn_sdot4(qh, wy, zc * ws, false), false);
   }
+  // wave sums by DPP (quad xor 1 / 2, half-row and row mirrors, row
+  // broadcasts 15 / 31): the total lands in lane 63; 16 independent chains
+  // interleave (ds_bpermute-based shuffles cost an LDS round trip each)
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0xB1, 0xF, 0xF, false);
 #pragma unroll
-    for (int o = 0; o < FC_N2; ++o) sacc[o] += __shfl_xor(sacc[o], off);
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x4E, 0xF, 0xF, false);
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x141, 0xF, 0xF, false);
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x140, 0xF, 0xF, false);
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x142, 0xA, 0xF, false);
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x143, 0xC, 0xF, false);
   int mine = 0;
 #pragma unroll
-  for (int o = 0; o < FC_N2; ++o)
-    if (lane == o) mine = sacc[o];
+  for (int o = 0; o < FC_N2; ++o) {
+    const int tot = __builtin_amdgcn_readlane(sacc[o], 63);
+    if (lane == o) mine = tot;
+  }
   if (lane < hd.n2) {
     const int o = lane;
     const int q2 = requant_one(mine, hd.u2[o], hd.v2[o], hd.m2[o], hd.z2, hd.lo2);
