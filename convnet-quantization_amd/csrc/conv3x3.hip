@@ -899,43 +899,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   uint8_t* in8_0 = lds + L::OFF_IN;
   uint8_t* in8_1 = lds + L::OFF_IN + L::IN8;
 
-  // ---- once per workgroup: resident conv2 weights (ring layout), epilogue
-  // constants of both layers, the patch column halos of both buffers
-  for (int e = tid; e < L::WRES / 16; e += 512) {
-    const int o = e * 16;
-    const int ch = o / C::WBUF, oc = o % C::WBUF;
-    const int r = oc >> 6, sl = (oc >> 4) & 3;
-    *reinterpret_cast<uint4*>(lds + L::OFF_W + o) = *reinterpret_cast<const uint4*>(
-        w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4));
-  }
-  stage_epik<64, 512>(ep1, reinterpret_cast<float*>(lds + L::OFF_EPI1), tid);
-  stage_epik<64, 512>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
-  if (tid < 16)
-    reinterpret_cast<int4*>(lds + L::OFF_CORR2)[tid] = reinterpret_cast<const int4*>(ep2.corr)[tid];
-  if (tid >= 64 && tid < 80)
-    reinterpret_cast<int4*>(lds + L::OFF_CORR1)[tid - 64] = reinterpret_cast<const int4*>(ep1.corr)[tid - 64];
-  if (wave == 4) {
-    // conv1 A operand in the dword-per-tap K order (k' = 4 tap + c, taps
-    // 0..7) from the [64][32] (k = 3 tap + c) packing
-    const int l32 = lane & 31, hi = lane >> 5;
-    v4i* a1t = reinterpret_cast<v4i*>(lds + L::OFF_A1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint4 r0 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32);
-      const uint4 r1 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32 + 16);
-      const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-      auto byte = [&](int k) -> uint32_t { return (wd[k >> 2] >> (8 * (k & 3))) & 0xff; };
-      auto tapw = [&](int t) -> int {   // (w[3t], w[3t+1], w[3t+2], 0)
-        return (int)(byte(3 * t) | (byte(3 * t + 1) << 8) | (byte(3 * t + 2) << 16));
-      };
-      // tap 8's three channels ride in the pad byte (byte 3) of taps 0, 1, 2,
-      // so the whole 27-long K fits one K=32 MFMA step
-      const v4i lo4 = (v4i){tapw(0) | (int)(byte(24) << 24), tapw(1) | (int)(byte(25) << 24),
-                            tapw(2) | (int)(byte(26) << 24), tapw(3)};
-      const v4i hi4 = (v4i){tapw(4), tapw(5), tapw(6), tapw(7)};
-      a1t[i * 64 + lane] = hi ? hi4 : lo4;
-    }
-  }
+  float4 xraw[3];
+  int xrow_ok = 0;
   const uint32_t padw = xor80(splat_u8(x2_zp));
   const uint4 pad4 = make_uint4(padw, padw, padw, padw);
   for (int e = tid; e < 2 * C::PROWS * 8; e += 512) {
@@ -944,7 +909,63 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     *reinterpret_cast<uint4*>(lds + buf * L::PATCH + C::slot(0, pr, pc) + chunk * 16) = pad4;
   }
 
-  float4 xraw[3];
+  // tables the tile loop reads (issued after the producer's first window
+  // loads, so the two latencies overlap); run by the consumer waves
+  auto setup = [&]() {
+    // ---- once per workgroup: resident conv2 weights (ring layout), epilogue
+    // constants of both layers, conv1's operand tables.  The weights go by
+    // LDS-DMA (9 x 1 KB per consumer wave); the producer waves only load
+    // their first input window meanwhile
+#ifndef QCN_EXP_SYNCW
+    if (!producer) {
+      const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+      for (int i = 0; i < L::WRES / 4096; ++i) {
+        const int p = i * 4 + wave_u;
+        const int o = p * 1024 + lane * 16;
+        const int ch = o / C::WBUF, oc = o % C::WBUF;
+        const int r = oc >> 6, sl = (oc >> 4) & 3;
+        glds16(w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), lds + L::OFF_W + p * 1024);
+      }
+    }
+#else
+    for (int e = tid; e < L::WRES / 16; e += 512) {
+      const int o = e * 16;
+      const int ch = o / C::WBUF, oc = o % C::WBUF;
+      const int r = oc >> 6, sl = (oc >> 4) & 3;
+      *reinterpret_cast<uint4*>(lds + L::OFF_W + o) = *reinterpret_cast<const uint4*>(
+          w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4));
+    }
+#endif
+    if (!producer) stage_epik<64, 256>(ep1, reinterpret_cast<float*>(lds + L::OFF_EPI1), tid);
+    if (!producer) stage_epik<64, 256>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
+    if (tid < 16)
+      reinterpret_cast<int4*>(lds + L::OFF_CORR2)[tid] = reinterpret_cast<const int4*>(ep2.corr)[tid];
+    if (tid >= 64 && tid < 80)
+      reinterpret_cast<int4*>(lds + L::OFF_CORR1)[tid - 64] = reinterpret_cast<const int4*>(ep1.corr)[tid - 64];
+    if (wave == 3) {
+      // conv1 A operand in the dword-per-tap K order (k' = 4 tap + c, taps
+      // 0..7) from the [64][32] (k = 3 tap + c) packing
+      const int l32 = lane & 31, hi = lane >> 5;
+      v4i* a1t = reinterpret_cast<v4i*>(lds + L::OFF_A1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint4 r0 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32);
+        const uint4 r1 = *reinterpret_cast<const uint4*>(w1 + (i * 32 + l32) * 32 + 16);
+        const uint32_t wd[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        auto byte = [&](int k) -> uint32_t { return (wd[k >> 2] >> (8 * (k & 3))) & 0xff; };
+        auto tapw = [&](int t) -> int {   // (w[3t], w[3t+1], w[3t+2], 0)
+          return (int)(byte(3 * t) | (byte(3 * t + 1) << 8) | (byte(3 * t + 2) << 16));
+        };
+        // tap 8's three channels ride in the pad byte (byte 3) of taps 0, 1, 2,
+        // so the whole 27-long K fits one K=32 MFMA step
+        const v4i lo4 = (v4i){tapw(0) | (int)(byte(24) << 24), tapw(1) | (int)(byte(25) << 24),
+                              tapw(2) | (int)(byte(26) << 24), tapw(3)};
+        const v4i hi4 = (v4i){tapw(4), tapw(5), tapw(6), tapw(7)};
+        a1t[i * 64 + lane] = hi ? hi4 : lo4;
+      }
+    }
+  };
   // Window staging, vectorised: producer thread pt < 180 owns window row
   // rr = pt / 9 and columns 4g-2 .. 4g+1 (g = pt % 9) of all three channels:
   // three 16-B loads (8-B aligned: dword-aligned is enough) and one 12-byte
@@ -960,7 +981,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     asm volatile("" : "+v"(v));
     return v;
   };
-  int xrow_ok = 0;
   auto stage_load = [&](int t) {
     const int n = t >> 1, y0 = (t & 1) * 16;
     const int pt = fresh_ptid();
@@ -1016,7 +1036,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   };
   bool vuni = false, muni = false;
   const bool fast1 = epi_fast(ep1);
-  auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb) {
+  // rows w, w + step, ... (of the 18 patch rows) of tile t
+  auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb, int w, int step) {
     // producer waves issue first: their VALU-bound conv1 is the longer phase,
     // the consumer's MFMAs fill the gaps (measured 53.6 vs 59.2 us)
     __builtin_amdgcn_s_setprio(QCN_PROD_PRIO);
@@ -1077,7 +1098,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           }
       }
       if constexpr (MODE == 0) {
-        for (int tr = wave - 4; tr < 18; tr += 4) {
+        for (int tr = w; tr < 18; tr += step) {
           const int iy = y0 - 1 + tr;
           uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
           if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
@@ -1099,8 +1120,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         // row's im2col reads and MFMAs are issued before this row's requant,
         // so the VALU never waits on an MFMA result (that cost ~40 s_nop per
         // row).  Halo rows are computed like the others and then overwritten.
-        const int w = wave - 4;
-        const int nr = w < 2 ? 5 : 4;
+        const int nr = (17 - w + step) / step;
         auto mfma_row = [&](int tr, v16i (&acc)[2]) {
           v4i b0;
           bop(tr, b0);
@@ -1173,11 +1193,11 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #pragma unroll
         for (int kr = 0; kr < 5; kr += 2) {
           if (kr >= nr) break;
-          if (kr + 1 < nr) mfma_row(w + 4 * (kr + 1), acc_y);
-          requant_row(acc_x, w + 4 * kr);
+          if (kr + 1 < nr) mfma_row(w + step * (kr + 1), acc_y);
+          requant_row(acc_x, w + step * kr);
           if (kr + 1 < nr) {
-            if (kr + 2 < nr) mfma_row(w + 4 * (kr + 2), acc_x);
-            requant_row(acc_y, w + 4 * (kr + 1));
+            if (kr + 2 < nr) mfma_row(w + step * (kr + 2), acc_x);
+            requant_row(acc_y, w + step * (kr + 1));
           }
         }
       }
@@ -1219,10 +1239,12 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   unsigned long long busy = 0, pa_ = 0, pb_ = 0, t_start = __builtin_amdgcn_s_memtime();
   if (tid == 0) qcn_stamps[blockIdx.x & 0xffff][6] = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (producer && T > 0) {
-    stage_load(tile_of(0));
-    stage_store(in8_0);
-  }
+  if (producer && T > 0) stage_load(tile_of(0));
+  setup();
+  if (producer && T > 0) stage_store(in8_0);
+#ifndef QCN_EXP_SYNCW
+  if (!producer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own weight DMA landed
+#endif
   __syncthreads();
   // conv1 requant specialisation: v (and mult) identical across channels —
   // per-tensor weights give v = 1/aws, mult = aws/s_y; per-channel v = 1
@@ -1235,6 +1257,11 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #ifdef QCN_STAMPS
   const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef QCN_EXP_NOSPLIT0
+  constexpr bool SPLIT0 = true;
+#else
+  constexpr bool SPLIT0 = false;
+#endif
   for (int j = 0; j <= T; ++j) {
 #ifdef QCN_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1246,7 +1273,12 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       const unsigned long long ta_ = __builtin_amdgcn_s_memtime();
       pa_ += ta_ - t0;
 #endif
-      if (j < T) conv1_tile(tile_of(j), (j & 1) ? in8_1 : in8_0, (j & 1) ? patch1 : patch0);
+      if (j < T) {
+        // the first tile's conv1 is split with the (otherwise idle) consumer waves
+        const bool split = SPLIT0 && j == 0;
+        conv1_tile(tile_of(j), (j & 1) ? in8_1 : in8_0, (j & 1) ? patch1 : patch0,
+                   split ? wave : wave - 4, split ? 8 : 4);
+      }
 #ifdef QCN_STAMPS
       const unsigned long long tb_ = __builtin_amdgcn_s_memtime();
       pb_ += tb_ - ta_;
@@ -1257,6 +1289,9 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #ifndef QCN_EXP_NOCONS
       conv2_tile(tile_of(j - 1), ((j - 1) & 1) ? patch1 : patch0);
 #endif
+    } else if (SPLIT0 && T > 0) {
+      conv1_tile(tile_of(0), in8_0, patch0, wave, 8);
+      __builtin_amdgcn_s_setprio(0);
     }
 #ifdef QCN_STAMPS
     busy += __builtin_amdgcn_s_memtime() - t0;
