@@ -9,8 +9,8 @@
 //     chunk-major ([K/32][rows][32]: conv6 writes its output that way, the
 //     weights are packed so at upload), so every fragment load is one
 //     contiguous 1 KB — row-major operands (4 KB row stride) ran 2-3x slower.
-//     Tiles are numbered XCD-major: the 32 workgroups of one XCD share one
-//     128-row block of X in that XCD's L2.  int32 partial sums go to a
+//     Each XCD takes one K quarter and half of the output tiles, so its L2
+//     holds a quarter of W and half of X's quarter.  int32 partial sums go to a
 //     workspace (4 x M x 512 x 4 B = 8 MB at batch 1024).
 //  2. fc_finish_kernel: one wave per row sums the partials, adds the
 //     zero-point correction, requantizes fc1 (+ReLU), writes the u8 fc1 row,
@@ -33,9 +33,26 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
                                                         int* __restrict__ part) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int MB = m / 128, NB = n / 64, T = MB * NB * FC_S;
-  int t = blockIdx.x;
-  if (T % 8 == 0) t = (t % 8) * (T / 8) + t / 8;   // XCD-major tile order
-  const int mb = t / (NB * FC_S), rem = t % (NB * FC_S), nb = rem / FC_S, s = rem % FC_S;
+  int mb, nb, s;
+  if (T % 8 == 0 && (MB * NB) % 2 == 0) {
+    // K-quarter-major over the XCDs (workgroup b runs on XCD b % 8): XCD x
+    // takes K quarter x % 4 and half (x / 4) of the (row block, feature
+    // block) tiles, so it fetches a quarter of W and half of X's K quarter:
+    // 1 MB per XCD at batch 1024 instead of 2.5 MB with row-block-major
+    // order (FETCH_SIZE 20.6 -> 8.3 MB, 9.27 -> 8.87 us)
+    const int x = blockIdx.x % 8, l = blockIdx.x / 8;
+    s = x % FC_S;
+    const int v = (x / FC_S) * (MB * NB / 2) + l;
+    mb = v / NB;
+    nb = v % NB;
+  } else {
+    int t = blockIdx.x;
+    if (T % 8 == 0) t = (t % 8) * (T / 8) + t / 8;   // row-block-major per XCD
+    mb = t / (NB * FC_S);
+    const int rem = t % (NB * FC_S);
+    nb = rem / FC_S;
+    s = rem % FC_S;
+  }
   const int mi = wave & 1, ni = wave >> 1;
   const int row0 = mb * 128 + mi * 64, col0 = nb * 64 + ni * 32;
   const int kcs = (k / 32) / FC_S, kc0 = s * kcs;
@@ -63,8 +80,13 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
       const uint4 a = f0[buf][u], b = f1[buf][u];
       const v4i b0 = (v4i){(int)xor80(a.x), (int)xor80(a.y), (int)xor80(a.z), (int)xor80(a.w)};
       const v4i b1 = (v4i){(int)xor80(b.x), (int)xor80(b.y), (int)xor80(b.z), (int)xor80(b.w)};
+#ifndef QCN_EXP_FC_NOMFMA
       acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b0, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b1, acc1, 0, 0, 0);
+#else   // diagnostic: loads only (results wrong by design)
+      acc0[u] ^= fw[buf][u][0] ^ b0[1];
+      acc1[u] ^= fw[buf][u][2] ^ b1[3];
+#endif
     }
   };
   load(0, 0);
@@ -78,6 +100,12 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
   const int l32 = lane & 31, hi = lane >> 5;
   int* pp = part + (long)s * m * n + col0 + 4 * hi;
   const int r = row0 + l32;
+#ifdef QCN_EXP_FC_NOSTORE   // diagnostic: no partial stores (results wrong by design)
+  int z = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) z ^= acc0[e] ^ acc1[e];
+  if (z != 0x12345678) return;
+#endif
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     *reinterpret_cast<int4*>(pp + (long)r * n + 8 * g) =

@@ -1236,7 +1236,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   };
 
 #ifdef QCN_STAMPS
-  unsigned long long busy = 0, pa_ = 0, pb_ = 0, t_start = __builtin_amdgcn_s_memtime();
+  unsigned long long busy = 0, bwait = 0, pa_ = 0, pb_ = 0, t_start = __builtin_amdgcn_s_memtime();
   if (tid == 0) qcn_stamps[blockIdx.x & 0xffff][6] = __builtin_amdgcn_s_memrealtime();
 #endif
   if (producer && T > 0) stage_load(tile_of(0));
@@ -1294,10 +1294,21 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       __builtin_amdgcn_s_setprio(0);
     }
 #ifdef QCN_STAMPS
-    busy += __builtin_amdgcn_s_memtime() - t0;
+    const unsigned long long tw = __builtin_amdgcn_s_memtime();
+    busy += tw - t0;
 #endif
     __syncthreads();
+#ifdef QCN_STAMPS
+    bwait += __builtin_amdgcn_s_memtime() - tw;
+#endif
   }
+#ifdef QCN_STAMPS
+  // per role: barrier wait, and the loop's elapsed time (waves 0 and 4)
+  if (tid == 0 || tid == 256) {
+    qcn_stamps[(blockIdx.x + 8192) & 0xffff][tid ? 1 : 0] = bwait;
+    qcn_stamps[(blockIdx.x + 8192) & 0xffff][tid ? 3 : 2] = __builtin_amdgcn_s_memtime() - t_pro;
+  }
+#endif
 #ifdef QCN_STAMPS
   // [0] start, [1] +prologue, [2] +consumer busy (wave 0), [3] +producer busy (wave 4), [5] end
   if (tid == 0) {

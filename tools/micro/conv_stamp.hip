@@ -35,6 +35,10 @@ static void report(const char* title, double macs, F launch) {
     double a = 0, b2 = 0; int cnt = 0;
     for (int b = 4096; b < 4096 + nwg; ++b) if (st[b][1]) { a += st[b][0]; b2 += st[b][1]; ++cnt; }
     if (cnt) printf("  producer per WG: stage_load %.0f, conv1 %.0f cycles\n", a / cnt, b2 / cnt);
+    double w0 = 0, w1 = 0, e0 = 0, e1 = 0; cnt = 0;
+    for (int b = 8192; b < 8192 + nwg; ++b) if (st[b][2]) { w0 += st[b][0]; w1 += st[b][1]; e0 += st[b][2]; e1 += st[b][3]; ++cnt; }
+    if (cnt) printf("  tile loop per WG: consumer wait %.0f of %.0f, producer wait %.0f of %.0f cycles\n",
+                    w0 / cnt, e0 / cnt, w1 / cnt, e1 / cnt);
   }
   if (nwg == 0) {
     printf("%s: %.2f us/launch (events), %.1f TOP/s (no stamps)\n", title, ms * 1e3,
