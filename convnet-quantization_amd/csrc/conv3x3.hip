@@ -881,8 +881,9 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
   }
 }
 
-// Tiles t0, t0 + ts, ..., (T of them; tile = half image) through the
-// producer/consumer pipeline.  512 threads, LDS layout Conv12P.
+// Images t0, t0 + ts, ... (T / 2 of them, each as its top then its bottom
+// half-image tile) through the producer/consumer pipeline.  512 threads, LDS
+// layout Conv12P.
 QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, int nimg,
                           float in_inv, int in_zp, const int8_t* __restrict__ w1, ConvEpi ep1,
                           int x2_zp, const int8_t* __restrict__ w2, ConvEpi ep2,
@@ -893,7 +894,9 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool producer = wave >= 4;
   const int ptid = tid - 256;
-  auto tile_of = [&](int j) { return t0 + j * ts; };
+  // tile j of this workgroup: image t0 + (j / 2) * ts, top half then bottom
+  // half (so every odd j reuses two conv1 rows from tile j - 1)
+  auto tile_of = [&](int j) { return (t0 + (j >> 1) * ts) * 2 + (j & 1); };
   uint8_t* patch0 = lds;
   uint8_t* patch1 = lds + L::PATCH;
   uint8_t* in8_0 = lds + L::OFF_IN;
@@ -1036,13 +1039,31 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   };
   bool vuni = false, muni = false;
   const bool fast1 = epi_fast(ep1);
-  // rows w, w + step, ... (of the 18 patch rows) of tile t
-  auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb, int w, int step) {
+  // conv2's patch for tile t: its 18 rows are conv1 rows y0 - 1 .. y0 + 16.
+  // The row outside the image (row 0 of a top half, row 17 of a bottom half)
+  // is conv2's zero-point padding, written without computing it.  A bottom
+  // half right after its top half (prev != nullptr) copies rows 0 and 1
+  // from rows 16 and 17 of the top half's patch (conv1 rows 15 and 16) instead
+  // of recomputing them.  The remaining rows are computed as r0 + w,
+  // r0 + w + step, ... (wave w of `step` waves).
+  auto conv1_tile = [&](int t, const uint8_t* in8, uint8_t* pb, const uint8_t* prev, int w,
+                        int step) {
     // producer waves issue first: their VALU-bound conv1 is the longer phase,
     // the consumer's MFMAs fill the gaps (measured 53.6 vs 59.2 us)
     __builtin_amdgcn_s_setprio(QCN_PROD_PRIO);
-    const int y0 = (t & 1) * 16;
+    const int h = t & 1, y0 = h * 16;
+    const int r0 = h == 0 ? 1 : (prev ? 2 : 0), r1 = h == 0 ? 18 : 17;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
+    if (w == step - 1) {   // the wave with the fewest rows: the padding row
+      uint8_t* prow_ptr = pb + C::slot(0, h == 0 ? 0 : 17, l32 + 1);
+      *reinterpret_cast<uint4*>(prow_ptr + hi * 32) = pad4;
+      *reinterpret_cast<uint4*>(prow_ptr + hi * 32 + 16) = pad4;
+    }
+    if (prev) {   // rows 16, 17 of the top half -> rows 0, 1 (whole rows, halos included)
+      for (int e = w * 64 + ln; e < 2 * C::RS / 16; e += step * 64)
+        *reinterpret_cast<uint4*>(pb + C::slot(0, 0, 0) + e * 16) =
+            *reinterpret_cast<const uint4*>(prev + C::slot(0, 16, 0) + e * 16);
+    }
     const float* ek1 = reinterpret_cast<const float*>(lds + L::OFF_EPI1);
     // conv1 A operand and corrected accumulator init from the LDS tables
     // (built once in the prologue; LDS latency instead of a dependent L2
@@ -1098,7 +1119,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           }
       }
       if constexpr (MODE == 0) {
-        for (int tr = w; tr < 18; tr += step) {
+        for (int tr = r0 + w; tr < r1; tr += step) {
           const int iy = y0 - 1 + tr;
           uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
           if (iy < 0 || iy >= 32) {  // wave-uniform: conv2's zero-point padding row
@@ -1120,7 +1141,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         // row's im2col reads and MFMAs are issued before this row's requant,
         // so the VALU never waits on an MFMA result (that cost ~40 s_nop per
         // row).  Halo rows are computed like the others and then overwritten.
-        const int nr = (17 - w + step) / step;
+        const int wr = r0 + w;   // first row of this wave
+        const int nr = (r1 - wr + step - 1) / step;
         auto mfma_row = [&](int tr, v16i (&acc)[2]) {
           v4i b0;
           bop(tr, b0);
@@ -1189,15 +1211,15 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         // v_mov_b64): row kr+1's im2col reads and MFMAs go out before row kr's
         // requant, so the VALU never waits on an MFMA result
         v16i acc_x[2], acc_y[2];
-        mfma_row(w, acc_x);
+        if (nr > 0) mfma_row(wr, acc_x);
 #pragma unroll
         for (int kr = 0; kr < 5; kr += 2) {
           if (kr >= nr) break;
-          if (kr + 1 < nr) mfma_row(w + step * (kr + 1), acc_y);
-          requant_row(acc_x, w + step * kr);
+          if (kr + 1 < nr) mfma_row(wr + step * (kr + 1), acc_y);
+          requant_row(acc_x, wr + step * kr);
           if (kr + 1 < nr) {
-            if (kr + 2 < nr) mfma_row(w + step * (kr + 2), acc_x);
-            requant_row(acc_y, w + step * (kr + 1));
+            if (kr + 2 < nr) mfma_row(wr + step * (kr + 2), acc_x);
+            requant_row(acc_y, wr + step * (kr + 1));
           }
         }
       }
@@ -1277,7 +1299,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         // the first tile's conv1 is split with the (otherwise idle) consumer waves
         const bool split = SPLIT0 && j == 0;
         conv1_tile(tile_of(j), (j & 1) ? in8_1 : in8_0, (j & 1) ? patch1 : patch0,
-                   split ? wave : wave - 4, split ? 8 : 4);
+                   (j & 1) ? patch0 : nullptr, split ? wave : wave - 4, split ? 8 : 4);
       }
 #ifdef QCN_STAMPS
       const unsigned long long tb_ = __builtin_amdgcn_s_memtime();
@@ -1290,7 +1312,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       conv2_tile(tile_of(j - 1), ((j - 1) & 1) ? patch1 : patch0);
 #endif
     } else if (SPLIT0 && T > 0) {
-      conv1_tile(tile_of(0), in8_0, patch0, wave, 8);
+      conv1_tile(tile_of(0), in8_0, patch0, nullptr, wave, 8);
       __builtin_amdgcn_s_setprio(0);
     }
 #ifdef QCN_STAMPS
@@ -1336,8 +1358,7 @@ __global__ __launch_bounds__(512, 1)
 void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
                     const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
                     const int8_t* __restrict__ w2, ConvEpi ep2, uint8_t* __restrict__ y) {
-  const int ntiles = 2 * nimg;
-  const int T = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int T = (int)blockIdx.x < nimg ? 2 * ((nimg - 1 - (int)blockIdx.x) / (int)gridDim.x + 1) : 0;
   conv12p_body((int)blockIdx.x, (int)gridDim.x, T, x, nimg, in_inv, in_zp, w1, ep1, x2_zp, w2, ep2, y);
 }
 
@@ -1376,7 +1397,7 @@ void net_kernel(NetArgs a) {
   static_assert(NetC3::NT == 512 && NetC5::NT == 512, "8-wave tiles");
   const int g = (int)blockIdx.x;   // one group of 4 images per workgroup
   if (a.phases & 1)
-    conv12p_body(8 * g, 1, 8, a.x, a.nimg, a.in_inv, a.in_zp, a.w1, a.ep1, a.x2_zp, a.w2, a.ep2, a.a2);
+    conv12p_body(4 * g, 1, 8, a.x, a.nimg, a.in_inv, a.in_zp, a.w1, a.ep1, a.x2_zp, a.w2, a.ep2, a.a2);
   // this workgroup's a2 stores have reached L2 before any wave re-reads them
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1667,7 +1688,7 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       return QCN_ERR_HIP;
   }
-  const int grid = 2 * nimg < ncu ? 2 * nimg : ncu;   // persistent: one workgroup per CU
+  const int grid = nimg < ncu ? nimg : ncu;   // persistent: one workgroup per CU
   hipLaunchKernelGGL(qcn::conv12p_kernel, dim3(grid), dim3(512), qcn::Conv12P::LDS,
                      (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
                      w2_packed, ep2, y);
