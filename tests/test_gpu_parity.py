@@ -346,11 +346,61 @@ def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
     assert torch.equal(y1, y1_ref)
     assert torch.equal(y2, y2_ref)
     assert torch.equal(y2f, y2f_ref)
+    # the workspace's row-block arrival counters stay valid across launches
+    # and batch sizes (the last workgroup of each row block writes the logits)
+    for mm in (m, 128, m, m):
+        y2.zero_()
+        y2f.zero_()
+        assert ops.classifier(ops.to_kmajor(T(qx[:mm])), l1, l2, ws, y1[:mm], y2[:mm], y2f[:mm])
+        torch.cuda.synchronize()
+        assert torch.equal(y2[:mm], y2_ref[:mm]) and torch.equal(y2f[:mm], y2f_ref[:mm])
     # fc1 against the numpy oracle on a slice (A9 numerics)
     want = qref.linear_q(qx[:32], zx, w1, u1, v1, m1, z1, True)
     assert np.array_equal(y1[:32].cpu().numpy(), want)
     # outside the envelope -> QCN_ERR_UNSUPPORTED -> False (caller falls back)
     assert not ops.classifier(ops.to_kmajor(T(qx[:100])), l1, l2, ws, y1, y2, y2f)
+
+
+def test_classifier_head_repeated_full_batch(dev):
+    """The one-launch head at batch 1024 (256 workgroups, XCD-grouped row
+    blocks, arrival counters): 20 back-to-back launches on one workspace, each
+    bit-identical to fc1 -> fc2 by the two static linear kernels."""
+    from types import SimpleNamespace as NS
+    from qconvnet import ops, quant as Q
+    rng = np.random.default_rng(21)
+    m, k, n1, n2 = 1024, 4096, 512, 10
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    qx = rng.integers(0, 256, (m, k), dtype=np.uint8)
+    w1 = rng.integers(-128, 128, (n1, k), dtype=np.int8)
+    w2 = rng.integers(-128, 128, (n2, n1), dtype=np.int8)
+    s_x, s_y1, s_y2, s_w1, s_w2 = F32(0.02), F32(0.05), F32(0.11), F32(2e-4), F32(2e-3)
+    b1 = rng.normal(0, 0.5, n1).astype(F32)
+    b2 = rng.normal(0, 0.5, n2).astype(F32)
+    zx, z1, z2 = 3, 0, 120
+    u1, v1, m1 = Q.epilogue_constants(s_x, s_w1, s_y1, b1)
+    u2, v2, m2 = Q.epilogue_constants(s_y1, s_w2, s_y2, b2)
+    corr1 = ((128 - zx) * w1.astype(np.int64).sum(1)).astype(np.int32)
+    corr2 = ((128 - z1) * w2.astype(np.int64).sum(1)).astype(np.int32)
+    y1_ref = ops.linear_u8(T(qx), zx, T(w1), T(u1), T(v1), T(m1), T(corr1), z1, True)
+    y2_ref, y2f_ref = ops.linear_u8(y1_ref, z1, T(w2), T(u2), T(v2), T(m2), T(corr2), z2, False,
+                                    y_scale=s_y2, want_fp32=True)
+    l1 = NS(w=T(w1), wk=T(ops.pack_fc_kmajor(w1)), u=T(u1), v=T(v1), mult=T(m1), corr=T(corr1),
+            z_y=z1, relu=True)
+    l2 = NS(w=T(w2), u=T(u2), v=T(v2), mult=T(m2), z_y=z2, relu=False, s_y=s_y2)
+    ws = ops.classifier_workspace(m, n1, dev)
+    xk = ops.to_kmajor(T(qx))
+    outs = []
+    for _ in range(20):
+        y1 = torch.empty((m, n1), dtype=torch.uint8, device=dev)
+        y2 = torch.empty((m, n2), dtype=torch.uint8, device=dev)
+        y2f = torch.empty((m, n2), dtype=torch.float32, device=dev)
+        assert ops.classifier(xk, l1, l2, ws, y1, y2, y2f)
+        outs.append((y1, y2, y2f))
+    torch.cuda.synchronize()
+    for y1, y2, y2f in outs:
+        assert torch.equal(y1, y1_ref)
+        assert torch.equal(y2, y2_ref)
+        assert torch.equal(y2f, y2f_ref)
 
 
 @pytest.mark.parametrize("pool", [True, False])
