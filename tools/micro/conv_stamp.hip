@@ -72,6 +72,19 @@ static void report(const char* title, double macs, F launch) {
          starts[nwg / 4], starts[nwg / 2], starts[3 * nwg / 4], starts[9 * nwg / 10], starts[nwg - 1]);
   printf("  WG end   (ns) pct 0/25/50/75/90/100: %.0f %.0f %.0f %.0f %.0f %.0f\n", ends[0],
          ends[nwg / 4], ends[nwg / 2], ends[3 * nwg / 4], ends[9 * nwg / 10], ends[nwg - 1]);
+  // per XCD (workgroup b on XCD b % 8): mean workgroup duration, mean clock,
+  // last end
+  printf("  per XCD: mean WG us | GHz | last end us:");
+  for (int x = 0; x < 8; ++x) {
+    double d = 0, g = 0, e = 0; int c = 0;
+    for (int b = x; b < nwg; b += 8) {
+      const double rt = (double)(st[b][7] - st[b][6]) * 10.0;
+      d += rt; g += (double)(st[b][5] - st[b][0]) / rt;
+      e = std::max(e, (double)(st[b][7] - r0) * 10.0); ++c;
+    }
+    if (c) printf("  [%d] %.1f %.2f %.1f", x, d / c / 1e3, g / c, e / 1e3);
+  }
+  printf("\n");
 }
 
 static unsigned rng = 12345;
