@@ -180,7 +180,7 @@ int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, i
 
 /* A9 x 2 + A7 — the static classifier head in two launches: fc1 (+ReLU)
  * u8 x s8 -> u8 [m, n1] as a 4-way split-K GEMM into an int32 workspace, then
- * one wave per row finishes fc1 (requant) and computes fc2 (n2 <= 64) and its
+ * one wave per row finishes fc1 (requant) and computes fc2 (n2 <= 16) and its
  * DeQuantStub.  Same results as qcn_linear_u8s8(fc1) followed by
  * qcn_linear_u8s8(fc2, y_deq) — fc2's input zero point is y1_zp, fc2's
  * correction is applied exactly in the finisher (no corr2 argument).
