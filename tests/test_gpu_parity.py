@@ -291,16 +291,19 @@ def test_batch_split_invariance_and_graph(dev):
     assert torch.equal(out, torch.flip(full, [0]))
 
 
-@pytest.mark.parametrize("mode", ["static", "qdq"])
-def test_fused_conv12_equals_unfused(dev, mode):
+@pytest.mark.parametrize("mode,n", [("static", 37), ("qdq", 37), ("static", 300), ("static", 1024),
+                                    ("qdq", 1024)])
+def test_fused_conv12_equals_unfused(dev, mode, n):
     """The fused conv1+conv2 launch produces the unfused pair's u8 output
-    exactly (odd batch: last workgroup pair partially outside the batch)."""
+    exactly.  37 images: fewer than the CUs, one image per workgroup; 300:
+    workgroups with two images and with one; 1024: four images per workgroup,
+    every bottom half reusing two conv1 rows of its top half."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
     from oracle import torch_ref
     z = netfix.load(False)
     spec = netfix.static_spec(z)[0] if mode == "static" else netfix.qdq_spec(z)
-    x = torch.from_numpy(torch_ref.synthetic_images(37, 9) * 1.5).to(dev)
+    x = torch.from_numpy(torch_ref.synthetic_images(n, 9) * 1.5).to(dev)
     a = QuantizedConvNet(spec, dev, fuse12=False).run(x, keep=True)[1]["a2"].clone()
     b = QuantizedConvNet(spec, dev, fuse12=True).run(x, keep=True)[1]["a2"].clone()
     torch.cuda.synchronize()
