@@ -893,7 +893,13 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool producer = wave >= 4;
+  // window-staging thread id: producer waves 5-7 (0..191, 180 used).  Wave 4
+  // computes the most conv1 rows of a top half (5 of 17), so it stages none
+#ifndef QCN_EXP_STAGE_W4
+  const int ptid = tid - 320;
+#else
   const int ptid = tid - 256;
+#endif
   // tile j of this workgroup: image t0 + (j / 2) * ts, top half then bottom
   // half (so every odd j reuses two conv1 rows from tile j - 1)
   auto tile_of = [&](int j) { return (t0 + (j >> 1) * ts) * 2 + (j & 1); };
@@ -985,11 +991,12 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     return v;
   };
   auto stage_load = [&](int t) {
+    if (ptid < 0) return;   // wave 4 (whole wave): no window share
     const int n = t >> 1, y0 = (t & 1) * 16;
     const int pt = fresh_ptid();
     const int rr = pt / 9, g = pt % 9;
     const int iy = y0 - 2 + rr, c0 = 4 * g - 2;
-    const bool row_ok = pt < 180 && iy >= 0 && iy < 32;
+    const bool row_ok = pt >= 0 && pt < 180 && iy >= 0 && iy < 32;
     xrow_ok = row_ok;
     // columns c0..c0+3 lie in [0, 32) except for g = 0 (c0 = -2) and g = 8 (c0 = 30):
     // load from a clamped in-row start, select per element at store time
@@ -1004,7 +1011,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   };
   auto stage_store = [&](uint8_t* in8) {  // quantize (aten quantize_per_tensor) -> s8
     const int pt = fresh_ptid();
-    if (pt < 180) {
+    if (pt >= 0 && pt < 180) {
       const int rr = pt / 9, g = pt % 9;
       const int c0 = 4 * g - 2;
       const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
