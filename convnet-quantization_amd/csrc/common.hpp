@@ -18,6 +18,27 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 
 #define QCN_DEV __device__ __forceinline__
 
+// Host-side, once per device: the dynamic-LDS limit of a kernel.  Launchers
+// run on the caller's current device (the Python side enters the model's
+// device first), so a flag per device id keeps a second GPU from launching
+// with an attribute only set on the first.
+constexpr int QCN_MAX_DEV = 64;
+inline int qcn_current_device() {
+  int d = 0;
+  return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < QCN_MAX_DEV) ? d : -1;
+}
+inline bool qcn_set_lds_once(const void* kernel, int lds_bytes, bool (&done)[QCN_MAX_DEV]) {
+  const int d = qcn_current_device();
+  if (d < 0) return false;
+  if (!done[d]) {
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes) !=
+        hipSuccess)
+      return false;
+    done[d] = true;
+  }
+  return true;
+}
+
 QCN_DEV int requant_one(int acc, float u, float v, float mult, int zp, int lo) {
   float a = (float)acc;                      // v_cvt_f32_i32: RNE, like cvtdq2ps
   float t = __builtin_fmaf(u, v, a);

@@ -1370,56 +1370,6 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
 }
 
 // --------------------------------------------------------------------------
-// The whole conv stack of the static int8 SimpleConvNet in one launch: each
-// workgroup (one per CU, LDS-bound) takes a group of 4 images through
-// conv1+conv2 (8 half-image tiles, producer/consumer pipeline), conv3+conv4
-// (two 2-image tiles, 8 waves) and conv5+conv6 (one 4-image tile), writing
-// a2 / a4 to HBM and re-reading them itself (L2-hot, same XCD, nt loads past
-// the L1).  Images are independent, so no workgroup ever waits for another:
-// no kernel boundaries (their tails and the all-CU HBM bursts of each
-// prologue), no launch gaps.
-using NetC3 = ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false>;
-using NetC4 = ConvCfg<128, 128, 16, true, 4, 16, 32, 0, true>;
-using NetC5 = ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>;
-using NetC6 = ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>;
-
-struct NetArgs {
-  const float* x; int nimg; float in_inv; int in_zp;
-  const int8_t* w1; ConvEpi ep1; int x2_zp; const int8_t* w2; ConvEpi ep2;
-  uint8_t* a2;
-  const int8_t* w3; ConvEpi ep3; int x3_zp; int x4_zp; const int8_t* w4; ConvEpi ep4;
-  uint8_t* a4;
-  const int8_t* w5; ConvEpi ep5; int x5_zp; int x6_zp; const int8_t* w6; ConvEpi ep6;
-  uint8_t* y;
-  int phases;   // diagnostic: bit 0 conv1+2, bit 1 conv3+4, bit 2 conv5+6 (QCN_NET_PHASES; 7 = all)
-};
-
-constexpr int net_lds_bytes() {
-  constexpr int a = Conv12P::LDS, b = PairCfg<NetC3, NetC4>::LDS, c = PairCfg<NetC5, NetC6>::LDS;
-  return a > b ? (a > c ? a : c) : (b > c ? b : c);
-}
-
-__global__ __launch_bounds__(512, 1)
-void net_kernel(NetArgs a) {
-  static_assert(NetC3::NT == 512 && NetC5::NT == 512, "8-wave tiles");
-  const int g = (int)blockIdx.x;   // one group of 4 images per workgroup
-  if (a.phases & 1)
-    conv12p_body(4 * g, 1, 8, a.x, a.nimg, a.in_inv, a.in_zp, a.w1, a.ep1, a.x2_zp, a.w2, a.ep2, a.a2);
-  // this workgroup's a2 stores have reached L2 before any wave re-reads them
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-#pragma unroll 1
-  for (int t = 0; t < ((a.phases & 2) ? 2 : 0); ++t) {
-    convpair_body<NetC3, NetC4, true>(2 * g + t, a.a2, a.nimg, a.x3_zp, a.w3, a.ep3, a.x4_zp, a.w4,
-                                      a.ep4, a.a4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  if (a.phases & 4)
-    convpair_body<NetC5, NetC6, true>(g, a.a4, a.nimg, a.x5_zp, a.w5, a.ep5, a.x6_zp, a.w6, a.ep6, a.y);
-}
-
-// --------------------------------------------------------------------------
 // Generic fallback (any CIN/COUT/H/W, no MFMA): one thread per output element.
 // Used only for shapes without a tuned instantiation (unit tests, odd sizes).
 __global__ void conv3x3_generic_kernel(const uint8_t* __restrict__ x, int nimg, int H, int W,
@@ -1478,13 +1428,8 @@ int launch_conv(const uint8_t* x, int nimg, int x_zp, const int8_t* wpk, const C
   const long pix = (long)nimg * C::IMG;
   const int grid = (int)((pix + C::PXB - 1) / C::PXB);
   auto k = conv3x3_u8s8_kernel<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
-        hipSuccess)
-      return QCN_ERR_HIP;
-    attr_done = true;
-  }
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, C::LDS, attr_done)) return QCN_ERR_HIP;
   hipLaunchKernelGGL(k, dim3(grid), dim3(C::NT), C::LDS, st, x, nimg, x_zp, wpk, ep, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
@@ -1496,13 +1441,8 @@ int launch_pair(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const Co
   const long pix = (long)nimg * CA::IMG;
   const int grid = (int)((pix + CA::PXB - 1) / CA::PXB);
   auto k = convpair_kernel<CA, CB>;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS) !=
-        hipSuccess)
-      return QCN_ERR_HIP;
-    attr_done = true;
-  }
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
   hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
@@ -1685,56 +1625,21 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   if (qdq1) { ep1.qdq = 1; ep1.s1 = qdq1->s1; ep1.z1 = qdq1->z1; ep1.inv2 = qdq1->inv2; ep1.z2 = qdq1->z2; }
   ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
   if (qdq2) { ep2.qdq = 1; ep2.s1 = qdq2->s1; ep2.z1 = qdq2->z1; ep2.inv2 = qdq2->inv2; ep2.z2 = qdq2->z2; }
-  static int ncu = 0;
-  if (!ncu) {
-    if (hipFuncSetAttribute((const void*)qcn::conv12p_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, qcn::Conv12P::LDS) != hipSuccess)
-      return QCN_ERR_HIP;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      return QCN_ERR_HIP;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  static int ncu_dev[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)qcn::conv12p_kernel, qcn::Conv12P::LDS, attr_done))
+    return QCN_ERR_HIP;
+  const int dev = qcn_current_device();
+  int& ncu = ncu_dev[dev];
+  if (!ncu && (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+               ncu <= 0)) {
+    ncu = 0;
+    return QCN_ERR_HIP;
   }
   const int grid = nimg < ncu ? nimg : ncu;   // persistent: one workgroup per CU
   hipLaunchKernelGGL(qcn::conv12p_kernel, dim3(grid), dim3(512), qcn::Conv12P::LDS,
                      (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
                      w2_packed, ep2, y);
-  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-}
-
-int qcn_convnet_static_u8(const float* x, int nimg, float in_scale, int in_zp,
-                          const qcn_conv_layer_t* layers, int kmajor, uint8_t* a2, uint8_t* a4,
-                          uint8_t* y, void* stream) {
-  if (!x || !layers || !a2 || !a4 || !y) return QCN_ERR_ARG;
-  if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
-  for (int i = 0; i < 6; ++i) {
-    const qcn_conv_layer_t& l = layers[i];
-    if (!l.w_packed || !l.u || !l.v || !l.mult || !l.corr) return QCN_ERR_ARG;
-    if (l.x_zp < 0 || l.x_zp > 255 || l.y_zp < 0 || l.y_zp > 255) return QCN_ERR_ARG;
-  }
-  if (nimg % 4 != 0) return QCN_ERR_UNSUPPORTED;   // groups of 4 images per workgroup
-  auto epi = [](const qcn_conv_layer_t& l, int km) {
-    return qcn::ConvEpi{l.u, l.v, l.mult, l.corr, l.y_zp, l.relu ? l.y_zp : 0, 0, 0.f, 0, 0.f, 0, km};
-  };
-  const qcn_conv_layer_t* L = layers;
-  qcn::NetArgs a{x, nimg, 1.0f / in_scale, in_zp,
-                 L[0].w_packed, epi(L[0], 0), L[1].x_zp, L[1].w_packed, epi(L[1], 0), a2,
-                 L[2].w_packed, epi(L[2], 0), L[2].x_zp, L[3].x_zp, L[3].w_packed, epi(L[3], 0), a4,
-                 L[4].w_packed, epi(L[4], 0), L[4].x_zp, L[5].x_zp, L[5].w_packed,
-                 epi(L[5], kmajor ? 1 : 0), y, 7};
-  static const int phases = [] {
-    const char* e = getenv("QCN_NET_PHASES");
-    return e ? atoi(e) : 7;
-  }();
-  a.phases = phases;
-  static bool attr_done = false;
-  if (!attr_done) {
-    if (hipFuncSetAttribute((const void*)qcn::net_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            qcn::net_lds_bytes()) != hipSuccess)
-      return QCN_ERR_HIP;
-    attr_done = true;
-  }
-  hipLaunchKernelGGL(qcn::net_kernel, dim3(nimg / 4), dim3(512), qcn::net_lds_bytes(), (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

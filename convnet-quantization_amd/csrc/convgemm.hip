@@ -389,12 +389,9 @@ int launch_gemm(GemmArgs& a, hipStream_t st) {
   using C = GemmCfg<BN>;
   a.mt = (int)((a.npix + C::BM - 1) / C::BM);
   a.nt = a.cout / BN;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_gemm_kernel<BN, RESID>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
-  }
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)conv_gemm_kernel<BN, RESID>, C::LDS, attr_done))
+    return QCN_ERR_HIP;
   hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID>), dim3(a.mt * a.nt), dim3(256), C::LDS, st, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from models.baseline_model import CONV_TABLE, SimpleConvNet, load_checkpoint_state
 from qconvnet import ops
 from qconvnet import quant as Q
-from qconvnet.qmodel import fold_state_dict
+from qconvnet.qmodel import cuda_device, fold_state_dict
 
 F32 = np.float32
 
@@ -36,7 +36,7 @@ class DynamicQuantConvNet:
     """fp32 convs (+ optional BN fold) and dynamic-int8 fc1/fc2 on the GPU."""
 
     def __init__(self, state_dict, fold=True, device="cuda", reduce_range=True):
-        self.device = torch.device(device)
+        self.device = cuda_device(device)
         self.reduce_range = reduce_range
         self.sharded = False   # True: batch-exact across ranks (see _range)
         self.quantized = True
@@ -80,6 +80,10 @@ class DynamicQuantConvNet:
 
     @torch.no_grad()
     def __call__(self, x):
+        with torch.cuda.device(self.device):   # ops launch on this device's current stream
+            return self._forward(x)
+
+    def _forward(self, x):
         host = not x.is_cuda
         x = x.to(self.device, torch.float32)
         for i, (w, b, bn) in enumerate(self.convs):
@@ -108,8 +112,7 @@ class DynamicQuantConvNet:
         return self
 
     def to(self, device):
-        if torch.device(device).type == "cpu":
-            self.host_io = True
+        self.host_io = torch.device(device).type == "cpu"   # compute stays on the GPU
         return self
 
     def cpu(self):

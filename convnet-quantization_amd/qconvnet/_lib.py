@@ -29,13 +29,6 @@ class QDQ(C.Structure):
     _fields_ = [("s1", C.c_float), ("z1", C.c_int32), ("inv2", C.c_float), ("z2", C.c_int32)]
 
 
-class ConvLayer(C.Structure):
-    """qcn_conv_layer_t"""
-    _fields_ = [("w_packed", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p),
-                ("mult", C.c_void_p), ("corr", C.c_void_p), ("x_zp", C.c_int32),
-                ("y_zp", C.c_int32), ("relu", C.c_int32)]
-
-
 vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_longlong
@@ -85,7 +78,6 @@ SIGNATURES = {
     "qcn_linear_dynamic_range_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp,
                                            vp]),
     "qcn_linear_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp]),
-    "qcn_convnet_static_u8": (i32, [vp, i32, f32, i32, C.POINTER(ConvLayer), i32, vp, vp, vp, vp]),
 }
 
 _lib = None

@@ -228,29 +228,6 @@ def conv_pair(x, la, lb, out, kmajor=False):
     return True
 
 
-def convnet_static(x, in_scale, in_zp, layers, a2, a4, out, kmajor=False):
-    """The six static int8 convs of SimpleConvNet (quantize + conv1 ... conv6
-    with their fused pools) in one persistent launch.  ``layers``: six objects
-    carrying w, u, v, mult, corr, z_x, z_y, relu.  a2 / a4: u8 workspaces
-    [n,16,16,64] / [n,8,8,128]; out: u8 [n,4,4,256] or chunk-major
-    [128,n,32] (kmajor).  Returns False when the batch is not a multiple of 4."""
-    _need(x, torch.float32, "convnet.x")
-    n = x.shape[0]
-    if tuple(x.shape[1:]) != (3, 32, 32):
-        raise ValueError("convnet_static expects [n,3,32,32]")
-    arr = (_lib.ConvLayer * 6)()
-    for i, lay in enumerate(layers):
-        arr[i] = _lib.ConvLayer(lay.w.data_ptr(), lay.u.data_ptr(), lay.v.data_ptr(),
-                                lay.mult.data_ptr(), lay.corr.data_ptr(), int(lay.z_x),
-                                int(lay.z_y), int(bool(lay.relu)))
-    rc = lib().qcn_convnet_static_u8(_ptr(x), n, float(in_scale), int(in_zp), arr,
-                                     int(bool(kmajor)), _ptr(a2), _ptr(a4), _ptr(out), _stream())
-    if rc == _lib.QCN_ERR_UNSUPPORTED:
-        return False
-    check(rc, "convnet_static")
-    return True
-
-
 def conv3x3_kmajor(x, x_zp, w_packed, cout, u, v, mult, corr, y_zp, relu, pool, out):
     """conv3x3 whose output is chunk-major [oh*ow*cout/32, n, 32] (conv6 -> fc1).
     Returns False when the shape is not supported (caller uses conv3x3)."""

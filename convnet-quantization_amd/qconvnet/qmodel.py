@@ -192,6 +192,15 @@ def qspec_from_torch_ao(q):
 
 
 # ============================================================ device model
+def cuda_device(device):
+    """torch.device with an explicit index ("cuda" -> the current device), so
+    launches can enter it and inputs can be checked against it."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError("the int8 path runs on the GPU (HIP); pass a cuda device")
+    return dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
+
+
 class _DevLayer:
     pass
 
@@ -203,19 +212,12 @@ class QuantizedConvNet:
     def __init__(self, spec, device="cuda", fuse12=True):
         self.spec = spec
         self.mode = spec["mode"]
-        self.device = torch.device(device)
-        if self.device.type != "cuda":
-            raise ValueError("the int8 path runs on the GPU (HIP); pass a cuda device")
+        self.device = cuda_device(device)
         self.quantized = True
         self.is_custom_quantized = self.mode == "qdq"
         self.host_io = False
         self.fuse12 = fuse12
         self.fuse_pairs = True
-        # one-launch conv stack (qcn_convnet_static_u8): correct, but measured
-        # slower than the three launches (177 vs 153 us at batch 1024: its
-        # conv3+conv4 phase runs both images of a group in one lockstep 8-wave
-        # workgroup, 73 vs 51 us); opt in with QCN_NET=1 or fuse_net = True
-        self.fuse_net = os.environ.get("QCN_NET", "0") == "1"
         self._bufs = {}
         self._graphs = {}
         self._upload()
@@ -296,8 +298,6 @@ class QuantizedConvNet:
         """Names of the launches run() marks, in order (conv1+conv2 are one
         launch when fused, conv3+conv4 / conv5+conv6 one launch each when
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
-        if self._net(x_shape, keep):
-            return ("net", "fc12") if self._head_fused(x_shape[0]) else ("net", "fc1", "fc2")
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
             names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
@@ -310,14 +310,6 @@ class QuantizedConvNet:
         activation stays in LDS); keep=True runs them per layer so every
         activation is inspectable."""
         return self.fuse_pairs and not keep and os.environ.get("QCN_PAIRS", "1") == "1"
-
-    def _net(self, x_shape, keep=False):
-        """The six static convs as one launch (qcn_convnet_static_u8): static
-        mode, 3x32x32 input, batch a multiple of 4, no per-layer QDQ; keep=True
-        runs the per-layer kernels so every activation is inspectable."""
-        return (self.fuse_net and self.fuse_pairs and self.fuse12 and not keep and
-                self.mode == "static" and tuple(x_shape[1:]) == (3, 32, 32) and
-                x_shape[0] % 4 == 0 and all(d.qdq is None for d in self.L))
 
     def _head_fused(self, n):
         f1, f2 = self.fc1, self.fc2
@@ -332,11 +324,18 @@ class QuantizedConvNet:
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
 
     def run(self, x, keep=False, marks=None):
-        """Launch the whole int8 forward on the current stream (no sync).
+        """Launch the whole int8 forward on the current stream of the model's
+        device (no sync).
         Returns the fp32 logits tensor (a reused buffer); with keep=True also
         the dict of intermediate u8 activations.  ``marks``: a list that
         receives one timing event before the first launch and one after each
         launch named by kernel_names(x.shape)."""
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        with torch.cuda.device(self.device):   # ops launch on this device's current stream
+            return self._run(x, keep, marks)
+
+    def _run(self, x, keep, marks):
         n = x.shape[0]
         b = self._buffers(n)
         L = self.L
@@ -351,19 +350,7 @@ class QuantizedConvNet:
         d = L[0]
         names = ["a2", "a3", "a4", "a5", "a6"]
         head = self._head_fused(n)
-        if self._net(x.shape, keep):
-            if head:
-                if "a6k" not in b:
-                    b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
-                out = b["a6k"]
-            else:
-                out = b["a6"]
-            if not ops.convnet_static(x, self.in_scale, self.in_zp, L, b["a2"], b["a4"], out,
-                                      kmajor=head):
-                raise RuntimeError("fused conv stack rejected a supported shape")
-            mark()
-            prev, first = out, 6
-        elif self._fused(x.shape):
+        if self._fused(x.shape):
             ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
             mark()
             prev, first = b["a2"], 2
@@ -479,9 +466,9 @@ class QuantizedConvNet:
         return self
 
     def to(self, device):
-        dev = torch.device(device)
-        if dev.type == "cpu":
-            self.host_io = True   # compute stays on the GPU; I/O is host tensors
+        # compute stays on the GPU; "cpu" only switches the I/O to host tensors,
+        # and moving back to cuda switches it back
+        self.host_io = torch.device(device).type == "cpu"
         return self
 
     def cpu(self):

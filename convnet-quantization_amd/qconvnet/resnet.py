@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 from . import ops
 from . import quant as Q
-from .qmodel import _DevLayer, _Range, _weight_scale
+from .qmodel import _DevLayer, _Range, _weight_scale, cuda_device
 
 F32 = np.float32
 
@@ -162,9 +162,7 @@ class QuantizedResNet:
 
     def __init__(self, spec, device="cuda"):
         self.spec = spec
-        self.device = torch.device(device)
-        if self.device.type != "cuda":
-            raise ValueError("the int8 path runs on the GPU (HIP); pass a cuda device")
+        self.device = cuda_device(device)
         self.quantized = True
         self.host_io = False
         self._graphs = {}
@@ -217,7 +215,14 @@ class QuantizedResNet:
         return out
 
     def run(self, x, keep=False, marks=None):
-        """The whole int8 forward on the current stream (no sync)."""
+        """The whole int8 forward on the current stream of the model's device
+        (no sync)."""
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        with torch.cuda.device(self.device):
+            return self._run(x, keep, marks)
+
+    def _run(self, x, keep, marks):
         inter = {}
 
         def mark(name):
@@ -311,8 +316,7 @@ class QuantizedResNet:
         return self
 
     def to(self, device):
-        if torch.device(device).type == "cpu":
-            self.host_io = True
+        self.host_io = torch.device(device).type == "cpu"   # compute stays on the GPU
         return self
 
     def cpu(self):

@@ -115,37 +115,6 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
                               const int32_t* corr2, int y_zp, int relu2, const qcn_qdq_t* qdq2,
                               uint8_t* y, void* stream);
 
-/* One static int8 conv layer of the whole-stack launch below (SURVEY §8(a)
- * A5/A6): packed s8 weights (conv1: qcn_pack_conv1_weight; conv2-6:
- * qcn_pack_conv3x3_weight), per-channel epilogue constants u / v / mult, the
- * zero-point correction corr = (128 - x_zp) * sum(w), input / output zero
- * points and the ReLU flag. */
-typedef struct qcn_conv_layer {
-  const int8_t* w_packed;
-  const float* u;
-  const float* v;
-  const float* mult;
-  const int32_t* corr;
-  int x_zp;
-  int y_zp;
-  int relu;
-} qcn_conv_layer_t;
-
-/* The six convolutions of the static int8 SimpleConvNet
- * (models/baseline_model.py:13-33 under torch.ao static PTQ; replaces the
- * conv part of the quantized model's forward, static_ptq_model.py /
- * custom_quantization_model.py) in ONE persistent launch: quantize_per_tensor
- * of the fp32 NCHW input (in_scale, in_zp), conv1 ... conv6 with the fused
- * 2x2 max-pools of conv2 / conv4 / conv6.  layers[6] as above.  Results are
- * bit-identical to qcn_conv12_fused_f32_nchw + two qcn_conv3x3_pair_u8s8.
- * a2: u8 [nimg,16,16,64] and a4: u8 [nimg,8,8,128] workspaces (written and
- * re-read inside the launch); y: conv6's pooled output, u8 NHWC
- * [nimg,4,4,256], or chunk-major [128][nimg][32] when kmajor.  nimg must be
- * a multiple of 4 (QCN_ERR_UNSUPPORTED otherwise). */
-int qcn_convnet_static_u8(const float* x, int nimg, float in_scale, int in_zp,
-                          const qcn_conv_layer_t* layers, int kmajor, uint8_t* a2, uint8_t* a4,
-                          uint8_t* y, void* stream);
-
 /* Two convolutions of one SimpleConvNet block in one launch: conv A
  * (cin -> cmid, no pool) then conv B (cmid -> cout, fused 2x2 max-pool).  A's
  * output never leaves LDS; the results are those of two qcn_conv3x3_u8s8_nhwc

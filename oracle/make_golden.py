@@ -303,6 +303,82 @@ def gen_net(per_channel=False, batch=64):
     return rec
 
 
+def _nchw_flat_to_nhwc(qflat, c=256, h=4):
+    """[n, c*h*h] in NCHW flatten order -> [n, h, h, c] (our conv6 layout)."""
+    return np.ascontiguousarray(qflat.reshape(-1, c, h, h).transpose(0, 2, 3, 1))
+
+
+def gen_net_headline(per_channel=False, batch=1024):
+    """BASELINE configs[2] (full static int8, batch 1024): the same model and
+    calibration as gen_net, run by torch.ao eager/fbgemm over 1024 images.
+    Records what the product's default launch sequence (conv12 -> conv34 ->
+    conv56 (chunk-major) -> fused classifier head) leaves in HBM: a2, a4, a6,
+    fc1 by hash, the u8 and fp32 logits in full."""
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    calib = tr.synthetic_images(512, 1)
+    fp = tr.reference_fp32_model(0, calib)
+    q = tr.build_static_int8_cpu(fp, [torch.from_numpy(calib)], per_channel=per_channel)
+    qm = extract_qmodel(q, per_channel)
+    x = tr.synthetic_images(batch, 0)
+    outs = {}
+    hooks = [getattr(q, f"conv{i}").register_forward_hook(
+        lambda m, a, o, k=i: outs.__setitem__(k, o)) for i in (2, 4, 6)]
+    hooks.append(q.fc1.register_forward_hook(lambda m, a, o: outs.__setitem__("fc1", o)))
+    hooks.append(q.fc2.register_forward_hook(lambda m, a, o: outs.__setitem__("fc2", o)))
+    with torch.no_grad():
+        ref = q(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    logits, ql, inter = qref.static_int8_forward(x, qm, keep=True)
+    assert (logits == ref).all(), "oracle != torch.ao static int8 at the headline batch"
+    rec = {"batch": np.int64(batch), "x_sha": sha(x), "logits": ref,
+           "q_logits": outs["fc2"].int_repr().numpy(), "argmax": qref.argmax_rows(ref),
+           "per_channel": np.int64(per_channel), "qm_in_scale": qm["in_scale"],
+           "qm_in_zp": np.int64(qm["in_zp"])}
+    assert (rec["q_logits"] == ql).all()
+    for i, a in ((2, "a2"), (4, "a4"), (6, "a6")):
+        o = qref.maxpool2x2_nhwc(outs[i].int_repr().permute(0, 2, 3, 1).contiguous().numpy())
+        assert (o == inter[f"conv{i}"]).all()
+        rec[f"{a}_sha"] = sha(o)
+    f1 = outs["fc1"].int_repr().numpy()
+    assert (f1 == inter["fc1"]).all()
+    rec["fc1_sha"] = sha(f1)
+    name = "net_static_int8_b1024_pc.npz" if per_channel else "net_static_int8_b1024.npz"
+    np.savez_compressed(os.path.join(OUT, name), **rec)
+    return rec
+
+
+def gen_qdq_config2(batch=256):
+    """BASELINE configs[1] (per-layer QDQ CustomQuantizedSimpleConvNet, batch
+    256): torch.ao's integer chain at every stub (each layer's input as the
+    next QuantStub quantizes it, NHWC, by hash) and fc1's u8 output, plus the
+    fp32 logits."""
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    calib = tr.synthetic_images(512, 1)
+    fp = tr.reference_fp32_model(0, calib)
+    qdq = tr.build_qdq_cpu(fp, [torch.from_numpy(calib)])
+    x = tr.synthetic_images(batch, 2)
+    outs = {}
+    hooks = [getattr(qdq, f"conv{i}").quant.register_forward_hook(
+        lambda m, a, o, k=i: outs.__setitem__(f"in{k}", o)) for i in range(1, 7)]
+    hooks.append(qdq.fc1.quant.register_forward_hook(lambda m, a, o: outs.__setitem__("in_fc1", o)))
+    hooks.append(qdq.fc1.op.register_forward_hook(lambda m, a, o: outs.__setitem__("fc1", o)))
+    with torch.no_grad():
+        ref = qdq(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    rec = {"batch": np.int64(batch), "x_sha": sha(x), "logits": ref, "argmax": qref.argmax_rows(ref)}
+    for i in range(2, 7):   # our a_{i-1} = conv_{i-1}'s QDQ hand-off = conv_i's quantized input
+        o = outs[f"in{i}"].int_repr().permute(0, 2, 3, 1).contiguous().numpy()
+        rec[f"a{i - 1}_sha"] = sha(o)
+    rec["a6_sha"] = sha(_nchw_flat_to_nhwc(outs["in_fc1"].int_repr().numpy()))
+    rec["fc1_sha"] = sha(outs["fc1"].int_repr().numpy())
+    np.savez_compressed(os.path.join(OUT, "net_qdq_b256.npz"), **rec)
+    return rec
+
+
 # ------------------------------------------- SURVEY §8(f)2 (ResNet blocks)
 def _convgen_case(rng, n, h, cin, cout, k, stride, pad, zx, relu, per_channel, zy):
     s_x = F32(rng.uniform(0.01, 0.03))
@@ -379,6 +455,11 @@ def main():
     if sys.argv[1:] == ["resnet"]:   # only the §8(f)2 vectors
         gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
         return
+    if sys.argv[1:] == ["headline"]:   # only the batch-1024 / batch-256 whole-net vectors
+        gen_net_headline(per_channel=False)
+        gen_net_headline(per_channel=True)
+        gen_qdq_config2()
+        return
     rng = np.random.Generator(np.random.PCG64(1234))
     gen_quantize(rng)
     gen_qparams(rng)
@@ -387,6 +468,9 @@ def main():
     gen_dynamic_linear(rng)
     gen_net(per_channel=False)
     gen_net(per_channel=True)
+    gen_net_headline(per_channel=False)
+    gen_net_headline(per_channel=True)
+    gen_qdq_config2()
     gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -1,0 +1,129 @@
+"""GPU parity at the BASELINE configs themselves (not at a reduced batch):
+
+* configs[2] — full static int8 at batch 1024: the DEFAULT launch sequence
+  bench.py times (conv12 -> conv34 -> conv56 with chunk-major output -> fused
+  classifier head) bit-exact to torch.ao eager static int8 (fbgemm) over the
+  same 1024 images (tests/golden/net_static_int8_b1024*.npz, written by
+  oracle/make_golden.py's gen_net_headline): a2, a4, conv6's chunk-major
+  output, fc1 by hash; u8 and fp32 logits in full;
+* configs[3]'s total batch (8192 = 8 x 1024) on one GPU: every 1024 shard
+  equals the 1024 run and the first shard equals the fixture;
+* configs[1] — the per-layer QDQ CustomQuantizedSimpleConvNet at batch 256
+  (tests/golden/net_qdq_b256.npz, gen_qdq_config2): every QuantStub's u8
+  hand-off and fc1's u8 output bit-exact, fp32 logits within 1e-5 relative
+  (fc2 is an fp32 GEMM whose summation order differs from MKL's)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HEADLINE = ("conv12", "conv34", "conv56", "fc12")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from qconvnet import _lib
+    _lib.load()
+    return torch.device("cuda:0")
+
+
+def _fixture(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name)))
+
+
+def _headline_model(per_channel, dev):
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load(per_channel)   # same model + calibration as the batch-1024 fixture
+    spec, _ = netfix.static_spec(z)
+    assert netfix.check_weights(spec, z) == []
+    return QuantizedConvNet(spec, dev)
+
+
+def _check_headline_bufs(model, n, z, rows=slice(None)):
+    import netfix
+    from qconvnet import ops
+    b = model._bufs[n]
+    assert netfix.sha(b["a2"][rows].cpu().numpy()) == str(z["a2_sha"])
+    assert netfix.sha(b["a4"][rows].cpu().numpy()) == str(z["a4_sha"])
+    a6 = ops.from_kmajor(b["a6k"])[rows].reshape(-1, 4, 4, 256)
+    assert netfix.sha(a6.cpu().numpy()) == str(z["a6_sha"])
+    assert netfix.sha(b["f1"][rows].cpu().numpy()) == str(z["fc1_sha"])
+    assert np.array_equal(b["q"][rows].cpu().numpy(), z["q_logits"])
+    assert np.array_equal(b["logits"][rows].cpu().numpy(), z["logits"])
+
+
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_headline_launch_sequence_equals_torchao(dev, golden_dir, per_channel):
+    import netfix
+    from oracle import torch_ref
+    z = _fixture(golden_dir, "net_static_int8_b1024_pc.npz" if per_channel else "net_static_int8_b1024.npz")
+    model = _headline_model(per_channel, dev)
+    assert (model.in_scale, model.in_zp) == (np.float32(z["qm_in_scale"]), int(z["qm_in_zp"]))
+    n = int(z["batch"])
+    x = torch_ref.synthetic_images(n, 0)
+    assert netfix.sha(x) == str(z["x_sha"])
+    xd = torch.from_numpy(x).to(dev)
+    assert model.kernel_names(xd.shape) == HEADLINE
+    model.run(xd)
+    torch.cuda.synchronize()
+    _check_headline_bufs(model, n, z)
+    # the HIP-graph replay of the same sequence
+    model.capture_graph(xd.clone())
+    out = model.replay(n)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), z["logits"])
+    assert np.array_equal(model(torch.from_numpy(x)).argmax(1).numpy(), z["argmax"])
+
+
+def test_batch_8192_shards_equal_1024(dev, golden_dir):
+    """configs[3]'s total batch on one GPU: the 8192 run equals its eight 1024
+    shards bit for bit (what each rank computes), and its first 1024 rows (the
+    same PCG64 stream) equal the torch.ao fixture."""
+    from oracle import torch_ref
+    z = _fixture(golden_dir, "net_static_int8_b1024.npz")
+    model = _headline_model(False, dev)
+    x = torch.from_numpy(torch_ref.synthetic_images(8192, 0)).to(dev)
+    assert model.kernel_names(x.shape) == HEADLINE
+    full = model.run(x).clone()
+    torch.cuda.synchronize()
+    _check_headline_bufs(model, 8192, z, rows=slice(0, 1024))
+    for r in range(8):
+        part = model.run(x[r * 1024:(r + 1) * 1024].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(part, full[r * 1024:(r + 1) * 1024]), r
+
+
+def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
+    import netfix
+    from oracle import torch_ref
+    from qconvnet.qmodel import QuantizedConvNet
+    z = _fixture(golden_dir, "net_qdq_b256.npz")
+    spec = netfix.qdq_spec(netfix.load(False))
+    n = int(z["batch"])
+    x = torch_ref.synthetic_images(n, 2)
+    assert netfix.sha(x) == str(z["x_sha"])
+    xd = torch.from_numpy(x).to(dev)
+    model = QuantizedConvNet(spec, dev)
+    names = model.kernel_names(xd.shape)
+    assert names[:3] == ("conv12", "conv34", "conv56"), names
+    tol = 1e-5 * np.abs(z["logits"]).max()
+    # default launches: a2, a4, a6, fc1 are the HBM hand-offs
+    logits = model.run(xd).cpu().numpy()
+    b = model._bufs[n]
+    for a in ("a2", "a4", "a6"):
+        assert netfix.sha(b[a].cpu().numpy()) == str(z[f"{a}_sha"]), a
+    assert netfix.sha(b["f1"].cpu().numpy()) == str(z["fc1_sha"])
+    assert np.abs(logits - z["logits"]).max() <= tol
+    assert np.array_equal(logits.argmax(1), z["argmax"])
+    # per-layer launches (keep=True, conv1 unfused): every stub's hand-off
+    m2 = QuantizedConvNet(spec, dev, fuse12=False)
+    logits2, b = m2.run(xd, keep=True)
+    for i in range(1, 7):
+        assert netfix.sha(b[f"a{i}"].cpu().numpy()) == str(z[f"a{i}_sha"]), i
+    assert np.array_equal(logits2.cpu().numpy(), logits)

@@ -476,40 +476,3 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     assert torch.equal(a6_p, a6_l)
     assert torch.equal(out_p, out_l)
     assert np.array_equal(out_p.cpu().numpy(), z["logits"])
-
-
-@pytest.mark.parametrize("per_channel", [False, True])
-def test_net_kernel_equals_launch_sequence(dev, per_channel):
-    """The six convs as ONE launch (qcn_convnet_static_u8: per-CU groups of 4
-    images through conv1+conv2, conv3+conv4, conv5+conv6, a2 / a4 re-read by
-    the writing CU) equal the separate conv12 + pair launches bit for bit:
-    a2, a4, the chunk-major conv6 output and the logits; a batch that is not
-    a multiple of 4 takes the separate launches."""
-    import netfix
-    from qconvnet import ops
-    from qconvnet.qmodel import QuantizedConvNet
-    from oracle import torch_ref
-    z = netfix.load(per_channel)
-    spec, _ = netfix.static_spec(z)
-    for n in (int(z["batch"]), 1024):
-        x = torch.from_numpy(torch_ref.synthetic_images(n, 5) if n == 1024 else netfix.images(z)).to(dev)
-        model = QuantizedConvNet(spec, dev)
-        model.fuse_net = True
-        assert model.kernel_names(x.shape)[0] == "net"
-        out_n = model.run(x).clone()
-        b = model._bufs[n]
-        a2_n, a4_n = b["a2"].clone(), b["a4"].clone()
-        a6_n = ops.from_kmajor(b["a6k"]).clone() if model._head_fused(n) else b["a6"].reshape(n, -1).clone()
-        model.fuse_net = False
-        assert model.kernel_names(x.shape)[0] == "conv12"
-        out_s = model.run(x).clone()
-        b = model._bufs[n]
-        a6_s = ops.from_kmajor(b["a6k"]) if model._head_fused(n) else b["a6"].reshape(n, -1)
-        torch.cuda.synchronize()
-        assert torch.equal(a2_n, b["a2"]), n
-        assert torch.equal(a4_n, b["a4"]), n
-        assert torch.equal(a6_n, a6_s), n
-        assert torch.equal(out_n, out_s), n
-    model = QuantizedConvNet(spec, dev)
-    model.fuse_net = True
-    assert model.kernel_names((37, 3, 32, 32))[0] == "conv12"

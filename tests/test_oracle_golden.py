@@ -89,6 +89,40 @@ def test_full_net_oracle(per_channel):
     assert np.array_equal(inter["conv1"][:2, :2, :2], z["conv1_slice"])
 
 
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_headline_fixture_oracle(golden_dir, per_channel):
+    """The batch-1024 fixture (configs[2]) is the same model and calibration
+    as the batch-64 one: same input qparams, its first 64 images are the
+    batch-64 images with the same logits, and the oracle reproduces a slice
+    of it (images 1000..1007)."""
+    import netfix
+    from oracle import torch_ref
+    z = netfix.load(per_channel)
+    h = _g(golden_dir, "net_static_int8_b1024_pc.npz" if per_channel else "net_static_int8_b1024.npz")
+    assert int(h["batch"]) == 1024
+    assert (F32(h["qm_in_scale"]), int(h["qm_in_zp"])) == (F32(z["qm_in_scale"]), int(z["qm_in_zp"]))
+    assert np.array_equal(h["q_logits"][:64], z["q_logits"])
+    assert np.array_equal(h["logits"][:64], z["logits"])
+    assert np.array_equal(h["argmax"], qref.argmax_rows(h["logits"]))
+    spec, _ = netfix.static_spec(z)
+    x = torch_ref.synthetic_images(1024, 0)
+    assert netfix.sha(x) == str(h["x_sha"])
+    logits, q, _ = qref.static_int8_forward(x[1000:1008], netfix.oracle_dict(spec), keep=True)
+    assert np.array_equal(q, h["q_logits"][1000:1008])
+    assert np.array_equal(logits, h["logits"][1000:1008])
+
+
+def test_qdq_config2_fixture(golden_dir):
+    """The batch-256 QDQ fixture (configs[1]) is self-consistent: its argmax
+    is the argmax of its logits, and its input is seed-2 synthetic data."""
+    import netfix
+    from oracle import torch_ref
+    h = _g(golden_dir, "net_qdq_b256.npz")
+    assert int(h["batch"]) == 256 and h["logits"].shape == (256, 10)
+    assert netfix.sha(torch_ref.synthetic_images(256, 2)) == str(h["x_sha"])
+    assert np.array_equal(h["argmax"], qref.argmax_rows(h["logits"]))
+
+
 def test_resnet_ops(golden_dir):
     """§8(f)2 ops: general convs (1x1, strided 3x3 / 1x1, 7x7/2 stem), the
     residual join and maxpool 3x3/2 against torch.ao / aten vectors."""
