@@ -20,9 +20,17 @@ StaticPTQModel path — torch.ao quantize_dynamic — timed on the host cores).
 from __future__ import annotations
 
 import argparse
+import contextlib
+import csv
+import glob
 import json
 import os
+import pickle
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -60,15 +68,23 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "conv56": 8 * 8 * 128 + 4 * 4 * 256,
                  "net": 3 * 32 * 32 * 4 + 4 * 4 * 256}
 HBM_BOUND = {"conv1"}
+# launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
+KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
+                  "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
+                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256",),
+                  "fc12": ("fc_splitk_kernel", "fc_finish_kernel")}
 
 
-def build_model(rank, device, per_channel=False):
+def build_model(rank, device, per_channel=False, spec_file=None):
     from models.baseline_model import trained_synthetic_model
     from qconvnet import data
     from qconvnet.dist import broadcast_object
     from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
     payload = None
-    if rank == 0:
+    if spec_file:   # a counter pass: the parent's model, written by this script
+        with open(spec_file, "rb") as f:
+            payload = pickle.load(f)
+    elif rank == 0:
         # trained on the synthetic 10-class task (no CIFAR-10 / checkpoint offline)
         x_cal, _ = data.synthetic_task(512, 1)
         calib = torch.from_numpy(x_cal)
@@ -89,26 +105,27 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
     fp.eval()
     threads = torch.get_num_threads()
     out = {}
-    # (1) StaticPTQModel as the reference builds it (static_ptq_model.py:19-34):
-    #     quantize_dynamic({Linear, Conv2d}, qint8) -> fp32 convs + dynamic int8 fc
+    # (1) BASELINE configs[0]: StaticPTQModel as the reference builds it
+    #     (static_ptq_model.py:19-34: quantize_dynamic({Linear, Conv2d}, qint8) ->
+    #     fp32 convs + dynamic int8 fc), timed on the CPU through the build's own
+    #     harness, InferenceBenchmark.measure_throughput(batch_size=32)
+    #     (utils/inference_benchmark.py:81-105), sized to ~`seconds` of CPU work
+    from utils.inference_benchmark import InferenceBenchmark
     sp = torch_ref.build_static_ptq_cpu(fp)
     bs = 32
     x = torch.from_numpy(data.synthetic_images(bs, 11))
-    with torch.no_grad():
-        for _ in range(3):
-            sp(x)
-        total, iters = 0.0, 0
-        while total < seconds:
-            t0 = time.time()
-            sp(x)
-            total += time.time() - t0
-            iters += 1
-    out["static_ptq"] = {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
+    harness = InferenceBenchmark([(x, torch.zeros(bs, dtype=torch.long))], device="cpu")
+    with contextlib.redirect_stdout(sys.stderr):   # stdout carries only the JSON line
+        harness.warm_up(sp, num_iterations=3)
+        probe = harness.measure_throughput(sp, batch_size=bs, num_iterations=20, verbose=False)
+        iters = max(20, int(seconds * probe / bs))
+        thr = harness.measure_throughput(sp, batch_size=bs, num_iterations=iters, verbose=False)
+    out["static_ptq"] = {"value": thr, "unit": "images/sec", "cores": threads,
                          "kind": "port",
-                         "sample": f"reference StaticPTQModel path (torch.ao quantize_dynamic "
-                                   f"{{Linear,Conv2d}} qint8 on our SimpleConvNet restatement), "
-                                   f"batch {bs} x {iters} iters, time.time() loop as "
-                                   f"utils/inference_benchmark.py:92-100"}
+                         "sample": f"BASELINE configs[0]: reference StaticPTQModel path (torch.ao "
+                                   f"quantize_dynamic {{Linear,Conv2d}} qint8 on our SimpleConvNet "
+                                   f"restatement), batch {bs} x {iters} iters through "
+                                   f"utils.inference_benchmark.InferenceBenchmark.measure_throughput"}
     # (2) full static int8 on the CPU (torch.ao eager, fbgemm) — apples to apples
     calib = torch.from_numpy(data.synthetic_task(512, 1)[0])   # the GPU model's calibration set
     q = torch_ref.build_static_int8_cpu(fp, [calib])
@@ -159,6 +176,115 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
     return out
 
 
+# ------------------------------------------------------------ PMC passes
+# HBM traffic, MFMA busy and the clock the chip holds come from rocprofv3
+# counter passes over a child run of this script (same model, same batch),
+# collected the way MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes:
+# one pass per counter group, FETCH_SIZE doubled on gfx950 (it tallies 128-B
+# requests at 64 B), WRITE_SIZE as is, both in KiB per dispatch; the clock as
+# GRBM_GUI_ACTIVE / 8 XCDs / kernel time on a batch-8192 dispatch (long enough
+# for the quotient to be accurate).
+PMC_PASSES = (("fetch", ("FETCH_SIZE",), None),
+              ("write", ("WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"), None),
+              ("clock", ("GRBM_GUI_ACTIVE",), 8192))
+
+
+def _pmc_child(counters, batch, spec_file, per_channel, timeout):
+    """One rocprofv3 --pmc pass over `bench.py --no-cpu --no-pmc` as a child
+    process (never an exec).  Returns ({kernel: {counter: mean per dispatch}},
+    the child's JSON line) or raises."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        raise RuntimeError("rocprofv3 not on PATH")
+    out = tempfile.mkdtemp(prefix="qcn_pmc_", dir="/tmp")
+    cmd = [exe, "--pmc", *counters, "--kernel-include-regex", "qcn::", "-f", "csv", "-d", out,
+           "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup",
+           "1", "--no-cpu", "--no-pmc", "--batch", str(batch), "--spec-file", spec_file]
+    if per_channel:
+        cmd.append("--per-channel")
+    env = dict(os.environ, TMPDIR="/tmp")
+    p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        shutil.rmtree(out, ignore_errors=True)
+        raise RuntimeError(f"rocprofv3 pass {counters} timed out")
+    try:
+        if p.returncode != 0:
+            raise RuntimeError(f"rocprofv3 pass {counters} exit {p.returncode}: {se[-400:]}")
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            raise RuntimeError(f"rocprofv3 pass {counters}: no counter csv")
+        agg = {}
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                d = agg.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], [])
+                d.append(float(r["Counter_Value"]))
+        child = next((json.loads(ln) for ln in so.splitlines() if ln.startswith("{")), None)
+        return {k: {c: float(np.mean(v)) for c, v in dd.items()} for k, dd in agg.items()}, child
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def _per_launch(agg, launch, counter):
+    """Sum over the launch's kernels of the mean per-dispatch counter value."""
+    tot, seen = 0.0, False
+    for sym in KERNEL_SYMBOLS[launch]:
+        for k, dd in agg.items():
+            if sym in k and counter in dd:
+                tot += dd[counter]
+                seen = True
+                break
+    return tot if seen else None
+
+
+def pmc_counters(model, sd, args, names, timeout=150):
+    """Counter passes for every launch; returns ({launch: {...}}, error text)."""
+    fd, spec_file = tempfile.mkstemp(prefix="qcn_spec_", suffix=".pkl", dir="/tmp")
+    with os.fdopen(fd, "wb") as f:
+        pickle.dump((model.spec, sd), f)
+    res = {n: {} for n in names}
+    errors = []
+    try:
+        for tag, counters, batch in PMC_PASSES:
+            try:
+                agg, child = _pmc_child(counters, batch or args.batch, spec_file, args.per_channel,
+                                        timeout)
+            except Exception as e:   # a failed pass leaves its fields null
+                errors.append(f"{tag}: {e}")
+                continue
+            for n in names:
+                if tag == "fetch":
+                    v = _per_launch(agg, n, "FETCH_SIZE")
+                    res[n]["fetch_bytes"] = None if v is None else 2.0 * v * 1024
+                elif tag == "write":
+                    v = _per_launch(agg, n, "WRITE_SIZE")
+                    res[n]["write_bytes"] = None if v is None else v * 1024
+                    busy = _per_launch(agg, n, "SQ_VALU_MFMA_BUSY_CYCLES")
+                    gui = _per_launch(agg, n, "GRBM_GUI_ACTIVE")
+                    res[n]["sq_valu_mfma_busy_cycles"] = busy
+                    res[n]["sq_insts_valu"] = _per_launch(agg, n, "SQ_INSTS_VALU")
+                    if busy is not None and gui:
+                        # per SIMD: busy cycles / (1024 SIMDs x dispatch cycles per XCD)
+                        res[n]["mfma_busy"] = busy / (1024.0 * gui / 8.0)
+                elif tag == "clock":
+                    gui = _per_launch(agg, n, "GRBM_GUI_ACTIVE")
+                    ms = (child or {}).get("kernels", {}).get(n, {}).get("ms")
+                    if gui and ms:
+                        res[n]["held_clock_ghz"] = gui / 8.0 / (ms * 1e-3) / 1e9
+                        res[n]["held_clock_batch"] = batch
+    finally:
+        os.unlink(spec_file)
+    for n in names:
+        r = res[n]
+        if r.get("fetch_bytes") is not None and r.get("write_bytes") is not None:
+            r["traffic_bytes"] = r["fetch_bytes"] + r["write_bytes"]
+    return res, "; ".join(errors) or None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +293,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 counter passes (traffic, MFMA busy, held clock)")
+    ap.add_argument("--spec-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--per-channel", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay the forward as one HIP graph (measured: no gain, the launch "
@@ -186,7 +315,7 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
 
-    model, sd = build_model(rank, dev, args.per_channel)
+    model, sd = build_model(rank, dev, args.per_channel, args.spec_file)
     B = args.batch
     x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
     gathered = torch.empty((world * B, 10), dtype=torch.float32, device=dev) if world > 1 else None
@@ -260,6 +389,23 @@ def main():
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": k["gbs"], "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": k["frac"], "traffic": None}
+    pmc_err = "skipped (--no-pmc or N > 1)"
+    if rank == 0 and world == 1 and not args.no_pmc:
+        pmc, pmc_err = pmc_counters(model, sd, args, names)
+        for n in names:
+            kern[n].update({kk: vv for kk, vv in pmc[n].items() if vv is not None})
+        p = pmc[dom]
+        roof["traffic"] = p.get("traffic_bytes")
+        roof["traffic_note"] = ("HBM bytes per launch from rocprofv3 --pmc passes of a child run "
+                                "(same model, batch): 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); "
+                                f"algorithmic bytes per launch {BYTES_PER_IMAGE[dom] * B}")
+        if p.get("mfma_busy") is not None:
+            roof["mfma_busy"] = p["mfma_busy"]
+        if p.get("held_clock_ghz"):
+            roof["held_clock_ghz"] = p["held_clock_ghz"]
+            roof["frac_at_held_clock"] = roof["achieved"] / (PEAK_INT8_TOPS * p["held_clock_ghz"] / 2.4)
+    if pmc_err:
+        roof["pmc_error"] = pmc_err
 
     result = {
         "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": world,

@@ -214,6 +214,31 @@ __global__ void argmax_kernel(const float* __restrict__ x, int rows, int cols,
   if (lane == 0) idx[wave] = bi;
 }
 
+// Inference BatchNorm1d (+ReLU) on [rows, cols] fp32, in ATen's CPU op order
+// (probed bit-exact against F.batch_norm(training=False) on the host):
+// y = fma(x, alpha[c], beta[c]) with alpha / beta precomputed on the host
+// (qconvnet.quant.bn_eval_affine).  One float4 of a row per lane.
+__global__ void channel_affine_kernel(const float* __restrict__ x, int rows, int cols,
+                                      const float* __restrict__ alpha,
+                                      const float* __restrict__ beta, int relu,
+                                      float* __restrict__ y) {
+  const int c4 = cols / 4;
+  const long long total = (long long)rows * c4;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % c4) * 4;
+    const float4 v = reinterpret_cast<const float4*>(x)[e];
+    const float4 a = *reinterpret_cast<const float4*>(alpha + c);
+    const float4 b = *reinterpret_cast<const float4*>(beta + c);
+    float4 o = make_float4(__builtin_fmaf(v.x, a.x, b.x), __builtin_fmaf(v.y, a.y, b.y),
+                           __builtin_fmaf(v.z, a.z, b.z), __builtin_fmaf(v.w, a.w, b.w));
+    if (relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    reinterpret_cast<float4*>(y)[e] = o;
+  }
+}
+
 }  // namespace qcn
 
 extern "C" {
@@ -286,6 +311,18 @@ int qcn_argmax_f32(const float* x, int rows, int cols, long long* idx, void* str
   const int blocks = (rows + 3) / 4;
   hipLaunchKernelGGL(qcn::argmax_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, rows,
                      cols, idx);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_channel_affine_f32(const float* x, int rows, int cols, const float* alpha,
+                           const float* beta, int relu, float* y, void* stream) {
+  if (!x || !alpha || !beta || !y || rows <= 0 || cols <= 0 || cols % 4) return QCN_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+       reinterpret_cast<uintptr_t>(alpha) | reinterpret_cast<uintptr_t>(beta)) & 15)
+    return QCN_ERR_ARG;
+  const long long work = (long long)rows * (cols / 4);
+  hipLaunchKernelGGL(qcn::channel_affine_kernel, dim3(qcn::grid_for(work, 256)), dim3(256), 0,
+                     (hipStream_t)stream, x, rows, cols, alpha, beta, relu, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

@@ -51,7 +51,10 @@ class DynamicQuantConvNet:
                       tuple(g[f"bn{i}.{k}"] for k in ("running_mean", "running_var", "weight", "bias")))
                      for i in range(1, 7)]
             fc1w, fc1b = g["fc1.weight"], g["fc1.bias"]
-            self.bn7 = tuple(self._t(g[f"bn7.{k}"]) for k in ("running_mean", "running_var", "weight", "bias"))
+            # bn7 in ATen's CPU op order (fma(x, alpha, beta')), so the dynamic
+            # fc2 sees bit-identical input to the reference's CPU model
+            self.bn7 = tuple(self._t(a) for a in Q.bn_eval_affine(
+                *(g[f"bn7.{k}"] for k in ("running_mean", "running_var", "weight", "bias"))))
         self.convs = [(self._t(w), self._t(b), tuple(self._t(a) for a in bn) if bn else None)
                       for w, b, bn in convs]
         self.fc = []
@@ -83,9 +86,8 @@ class DynamicQuantConvNet:
         with torch.cuda.device(self.device):   # ops launch on this device's current stream
             return self._forward(x)
 
-    def _forward(self, x):
-        host = not x.is_cuda
-        x = x.to(self.device, torch.float32)
+    def features(self, x):
+        """fp32 convs (+BN, ReLU, pools) -> the [N, 4096] NCHW-flatten fc1 input."""
         for i, (w, b, bn) in enumerate(self.convs):
             x = F.conv2d(x, w, b, padding=1)
             if bn is not None:
@@ -93,14 +95,26 @@ class DynamicQuantConvNet:
             x = F.relu(x)
             if CONV_TABLE[i][2]:
                 x = F.max_pool2d(x, 2, 2)
-        x = x.reshape(x.shape[0], -1).contiguous()
-        w, s, ws, b = self.fc[0]
-        x = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range, minmax=self._range(x))
-        if self.bn7 is not None:
-            x = F.batch_norm(x, self.bn7[0], self.bn7[1], self.bn7[2], self.bn7[3], False, 0.0, 1e-5)
-        x = F.relu(x).contiguous()
-        w, s, ws, b = self.fc[1]
-        y = ops.linear_dynamic(x, w, s, ws, b, self.reduce_range, minmax=self._range(x))
+        return x.reshape(x.shape[0], -1).contiguous()
+
+    @torch.no_grad()
+    def classify(self, feats):
+        """dynamic-int8 fc1 -> [bn7] -> ReLU -> dynamic-int8 fc2 on [N, 4096]
+        fp32 features (device tensor in, device logits out, no sync)."""
+        with torch.cuda.device(self.device):
+            w, s, ws, b = self.fc[0]
+            x = ops.linear_dynamic(feats, w, s, ws, b, self.reduce_range, minmax=self._range(feats))
+            if self.bn7 is not None:
+                x = ops.channel_affine(x, self.bn7[0], self.bn7[1], relu=True)
+            else:
+                x = F.relu(x).contiguous()
+            w, s, ws, b = self.fc[1]
+            return ops.linear_dynamic(x, w, s, ws, b, self.reduce_range, minmax=self._range(x))
+
+    def _forward(self, x):
+        host = not x.is_cuda
+        x = x.to(self.device, torch.float32)
+        y = self.classify(self.features(x))
         if host or self.host_io:
             return y.cpu()
         torch.cuda.current_stream(self.device).synchronize()

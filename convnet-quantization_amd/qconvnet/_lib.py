@@ -43,6 +43,7 @@ SIGNATURES = {
     "qcn_minmax_f32": (i32, [vp, i64, vp, vp]),
     "qcn_maxpool2x2_u8_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_argmax_f32": (i32, [vp, i32, i32, vp, vp]),
+    "qcn_channel_affine_f32": (i32, [vp, i32, i32, vp, vp, i32, vp, vp]),
     "qcn_conv3x3_packed_size": (i32, [i32, i32]),
     "qcn_pack_conv3x3_weight": (i32, [vp, i32, i32, vp, vp]),
     "qcn_pack_conv1_weight": (i32, [vp, i32, vp, vp]),

@@ -95,6 +95,18 @@ def argmax(x):
     return out
 
 
+def channel_affine(x, alpha, beta, relu=False, out=None):
+    """Inference BatchNorm1d (+ReLU) on [rows, cols] fp32: fma(x, alpha, beta)
+    per column (alpha / beta from quant.bn_eval_affine)."""
+    _need(x, torch.float32, "channel_affine.x")
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib().qcn_channel_affine_f32(_ptr(x), rows, cols, _ptr(alpha), _ptr(beta), int(bool(relu)),
+                                       _ptr(out), _stream()), "channel_affine")
+    return out
+
+
 # ------------------------------------------------------------------- packing
 def pack_conv3x3(w_oihw: np.ndarray):
     """Host packing of s8 OIHW weights -> (packed bytes, wsum int32)."""

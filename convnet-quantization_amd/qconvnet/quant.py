@@ -65,6 +65,22 @@ def fold_linear_bn(w, b, mean, var, gamma, beta, eps=1e-5):
     return wf, bf
 
 
+def bn_eval_affine(mean, var, gamma, beta, eps=1e-5):
+    """Per-channel (alpha, beta') of an inference BatchNorm in ATen's CPU op
+    order (torch 2.10 batch_norm with training=False, probed bit-exact on the
+    host): invstd = fp32(1 / sqrt(fp32(var + eps))), alpha = fp32(invstd *
+    gamma), beta' = fma(-mean, alpha, beta); then y = fma(x, alpha, beta')."""
+    f32 = np.float32
+    mean, var = np.asarray(mean, f32), np.asarray(var, f32)
+    gamma, beta = np.asarray(gamma, f32), np.asarray(beta, f32)
+    invstd = (f32(1.0) / np.sqrt(var + f32(eps))).astype(f32)
+    alpha = (invstd * gamma).astype(f32)
+    # the float64 product of two fp32 values is exact; one rounding to fp32
+    # after the add reproduces fma except in double-rounding corner cases
+    bprime = (beta.astype(np.float64) - mean.astype(np.float64) * alpha.astype(np.float64)).astype(f32)
+    return alpha, bprime
+
+
 def quantize_weight(w, scale):
     """q = clamp(rne(w * fp32(1/s)), -128, 127), per tensor (scalar scale) or per
     output channel (vector scale)."""

@@ -72,6 +72,14 @@ int qcn_maxpool2x2_u8_nhwc(const uint8_t* x, int n, int h, int w, int c, uint8_t
  * topk(1), utils/model_evaluator.py:36,96,160). */
 int qcn_argmax_f32(const float* x, int rows, int cols, long long* idx, void* stream);
 
+/* Inference BatchNorm1d (+ReLU) on fp32 [rows, cols] (bn7 of the reference's
+ * StaticPTQModel between its dynamic fc1 and fc2, models/static_ptq_model.py:
+ * 19-34 over baseline_model.py:80-82): y = fma(x, alpha[c], beta[c]), then
+ * max(y, 0) when relu, in ATen's CPU op order (alpha / beta from the host,
+ * qconvnet.quant.bn_eval_affine).  cols % 4 == 0, 16-B aligned pointers. */
+int qcn_channel_affine_f32(const float* x, int rows, int cols, const float* alpha,
+                           const float* beta, int relu, float* y, void* stream);
+
 /* A5/A6 weight packing (host).  w_oihw is torch's s8 [cout][cin][3][3].
  * out receives qcn_conv3x3_packed_size(cin, cout) bytes; wsum[cout] receives
  * sum_k w (for the activation zero-point correction). */

@@ -127,3 +127,18 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     for i in range(1, 7):
         assert netfix.sha(b[f"a{i}"].cpu().numpy()) == str(z[f"a{i}_sha"]), i
     assert np.array_equal(logits2.cpu().numpy(), logits)
+
+
+def test_model_on_second_device(golden_dir):
+    """A model built for cuda:1 runs there while cuda:0 is current (every
+    forward enters the model's device; kernel attributes are set per device)."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    from oracle import torch_ref
+    z = _fixture(golden_dir, "net_static_int8_b1024.npz")
+    torch.cuda.set_device(0)
+    model = _headline_model(False, torch.device("cuda:1"))
+    x = torch.from_numpy(torch_ref.synthetic_images(1024, 0)).to("cuda:1")
+    out = model.run(x)
+    torch.cuda.synchronize("cuda:1")
+    assert np.array_equal(out.cpu().numpy(), z["logits"])

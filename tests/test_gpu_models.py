@@ -67,27 +67,68 @@ def test_custom_quantization_model_qdq(z, sd):
     assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
-def test_dynamic_models_close_to_reference(z, sd):
-    """fp32 convs on the GPU differ from oneDNN in the last bits, so the dynamic
-    activation scales can move by an ulp: compare with a tolerance + argmax."""
-    import netfix
+def _cpu_reference(sd, kind):
+    """The reference's CPU model on THIS host: StaticPTQModel
+    (static_ptq_model.py:19-34, quantize_dynamic over the unfolded net) or
+    DynamicPTQModel (dynamic_ptq_model.py:281-308, BN folded first)."""
+    from oracle import torch_ref
+    fp = torch_ref.SimpleConvNetRef()
+    fp.load_state_dict(sd)
+    fp.eval()
+    return (torch_ref.build_static_ptq_cpu(fp) if kind == "static_ptq"
+            else torch_ref.build_dynamic_ptq_cpu(fp))
+
+
+def _gpu_reference_mode(sd, kind):
     from models.dynamic_ptq_model import DynamicPTQModel
     from models.static_ptq_model import StaticPTQModel
-    x = torch.from_numpy(netfix.images(z))
-    m = DynamicPTQModel()
+    m = StaticPTQModel(mode="reference") if kind == "static_ptq" else DynamicPTQModel()
     m.load_state_dict(sd)
-    m.quantize()
-    out = m(x).numpy()
-    ref = z["dynamic_ptq_logits"]
-    assert np.abs(out - ref).max() < 0.05 * np.abs(ref).max()
-    assert (out.argmax(1) == ref.argmax(1)).mean() >= 0.95
-    r = StaticPTQModel(mode="reference")
-    r.load_state_dict(sd)
-    q = r.quantize()
-    out = q(x).numpy()
-    ref = z["static_ptq_logits"]
-    assert np.abs(out - ref).max() < 0.05 * np.abs(ref).max()
-    assert (out.argmax(1) == ref.argmax(1)).mean() >= 0.95
+    return m.quantize()
+
+
+@pytest.mark.parametrize("kind", ["static_ptq", "dynamic_ptq"])
+def test_reference_mode_classifier_exact_on_cpu_features(z, sd, kind):
+    """Given the CPU model's own conv features (fc1's input), the GPU
+    reference-mode classifier (dynamic-int8 fc1 -> bn7 -> ReLU -> dynamic-int8
+    fc2, HIP kernels) reproduces the CPU logits bit for bit."""
+    import netfix
+    ref = _cpu_reference(sd, kind)
+    feats = {}
+    h = ref.fc1.register_forward_pre_hook(lambda m, a: feats.__setitem__("x", a[0].clone()))
+    x = torch.from_numpy(netfix.images(z))
+    with torch.no_grad():
+        want = ref(x).numpy()
+    h.remove()
+    if kind == "static_ptq":   # the fixture was written by the same CPU path here
+        np.testing.assert_allclose(want, z["static_ptq_logits"], rtol=0, atol=1e-3 * np.abs(want).max())
+    q = _gpu_reference_mode(sd, kind)
+    got = q.classify(feats["x"].cuda().contiguous()).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+# End to end, the fp32 convs run on MIOpen instead of oneDNN: features differ
+# in the last bits (measured max relative feature difference ~1e-6), which
+# moves a few dynamic-quantized fc inputs by one step.  Stated bound on the
+# logits: |d| <= 1 % of max|logit| (measured, test log: ~0.1-0.3 %), and
+# argmax agreement >= 99.9 % over 4096 images.
+REF_MODE_REL_TOL = 1e-2
+
+
+@pytest.mark.parametrize("kind", ["static_ptq", "dynamic_ptq"])
+def test_reference_mode_end_to_end(sd, kind):
+    from oracle import torch_ref
+    x = torch.from_numpy(torch_ref.synthetic_images(4096, 41))
+    ref = _cpu_reference(sd, kind)
+    q = _gpu_reference_mode(sd, kind)
+    with torch.no_grad():
+        want = torch.cat([ref(x[i:i + 512]) for i in range(0, 4096, 512)]).numpy()
+    got = np.concatenate([q(x[i:i + 512]).numpy() for i in range(0, 4096, 512)])
+    rel = np.abs(got - want).max() / np.abs(want).max()
+    agree = (got.argmax(1) == want.argmax(1)).mean()
+    print(f"{kind}: max rel diff {rel:.3e}, argmax agreement {agree * 100:.3f} %")
+    assert rel <= REF_MODE_REL_TOL
+    assert agree >= 0.999
 
 
 def test_dynamic_linear_exact_on_same_input(sd):

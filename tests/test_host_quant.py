@@ -117,3 +117,19 @@ def test_spec_from_torch_ao_matches_native_flow():
             assert np.array_equal(a[name][k], b[name][k]), (name, k)
         for k in ("s_x", "z_x", "s_y", "z_y"):
             assert a[name][k] == b[name][k], (name, k)
+
+
+def test_bn_eval_affine_matches_torch_cpu():
+    """bn7 of the reference StaticPTQModel runs in fp32 on the host;
+    fma(x, alpha, beta') with quant.bn_eval_affine's constants reproduces
+    F.batch_norm(training=False) bit for bit."""
+    import torch
+    from qconvnet import quant as Q
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(128, 512, generator=g) * 3
+    mean, var = torch.randn(512, generator=g), torch.rand(512, generator=g) + 0.05
+    w, b = torch.randn(512, generator=g), torch.randn(512, generator=g)
+    want = torch.nn.functional.batch_norm(x, mean, var, w, b, False, 0.0, 1e-5).numpy()
+    a, bp = Q.bn_eval_affine(mean.numpy(), var.numpy(), w.numpy(), b.numpy())
+    got = (x.numpy().astype(np.float64) * a.astype(np.float64) + bp.astype(np.float64)).astype(np.float32)
+    assert np.array_equal(got, want)

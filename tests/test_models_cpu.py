@@ -55,3 +55,52 @@ def test_static_ptq_wrapper_rejects_cpu_device():
     # calibration runs on the host, but the int8 model itself refuses the CPU
     with pytest.raises(ValueError):
         sp.quantize(torch.from_numpy(data.synthetic_images(8, 1)))
+
+
+class _FixedLogits:
+    """A model stand-in that returns a fixed logits table, one batch per call."""
+
+    def __init__(self, logits, batch):
+        self.logits, self.batch, self.i = logits, batch, 0
+
+    def eval(self):
+        return self
+
+    def cpu(self):
+        return self
+
+    def to(self, device):
+        return self
+
+    def __call__(self, x):
+        out = self.logits[self.i:self.i + x.shape[0]]
+        self.i += x.shape[0]
+        return out
+
+
+def test_model_evaluator_matches_numpy_topk():
+    """ModelEvaluator's top-1/top-5 (reference model_evaluator.py:36-41) and
+    per-class accuracy (:94-112) against a numpy restatement on the same
+    logits: top-k = the k largest, per-class = argmax (first max) == label."""
+    import numpy as np
+    from utils.model_evaluator import ModelEvaluator
+    rng = np.random.default_rng(11)
+    n, c, bs = 1000, 10, 128
+    logits = rng.standard_normal((n, c)).astype(np.float32)
+    labels = rng.integers(0, c, n)
+    x = torch.zeros(n, 1)
+    loader = [(x[i:i + bs], torch.from_numpy(labels[i:i + bs])) for i in range(0, n, bs)]
+    ev = ModelEvaluator(loader)
+    top1, top5 = ev.evaluate_accuracy(_FixedLogits(torch.from_numpy(logits), bs), verbose=False)
+    order = np.argsort(-logits, axis=1, kind="stable")
+    assert top1 == 100.0 * (order[:, 0] == labels).sum() / n
+    assert top5 == 100.0 * (order[:, :5] == labels[:, None]).any(1).sum() / n
+    classes = [f"class{i}" for i in range(c)]
+    got = ev.evaluate_class_accuracy(_FixedLogits(torch.from_numpy(logits), bs), classes, verbose=False)
+    pred = logits.argmax(1)
+    want = {classes[k]: 100.0 * ((pred == k) & (labels == k)).sum() / (labels == k).sum() for k in range(c)}
+    assert list(got) == sorted(want, key=lambda k: want[k], reverse=True)
+    for k, v in want.items():
+        assert abs(got[k] - v) < 1e-9
+    res = ev.compare_models({"m": _FixedLogits(torch.from_numpy(logits), bs)}, classes)
+    assert abs(res["m"]["accuracy"] - 100.0 * (pred == labels).sum() / n) < 1e-9
