@@ -108,10 +108,11 @@ def test_reference_mode_classifier_exact_on_cpu_features(z, sd, kind):
 
 
 # End to end, the fp32 convs run on MIOpen instead of oneDNN: features differ
-# in the last bits (measured max relative feature difference ~1e-6), which
-# moves a few dynamic-quantized fc inputs by one step.  Stated bound on the
-# logits: |d| <= 1 % of max|logit| (measured, test log: ~0.1-0.3 %), and
-# argmax agreement >= 99.9 % over 4096 images.
+# in the last bits, which moves a few dynamic-quantized fc inputs by one
+# step.  Stated bound on the logits: |d| <= 1 % of max|logit| (measured
+# 0.6 % on this random-init model).  Argmax may differ only where the CPU
+# model's own top-1 margin is inside that bound; over 4096 images >= 99.5 %
+# agree (measured 99.85 %: the 6 others all sit on near-ties).
 REF_MODE_REL_TOL = 1e-2
 
 
@@ -128,7 +129,11 @@ def test_reference_mode_end_to_end(sd, kind):
     agree = (got.argmax(1) == want.argmax(1)).mean()
     print(f"{kind}: max rel diff {rel:.3e}, argmax agreement {agree * 100:.3f} %")
     assert rel <= REF_MODE_REL_TOL
-    assert agree >= 0.999
+    top2 = np.sort(want, axis=1)[:, -2:]
+    margin = top2[:, 1] - top2[:, 0]
+    flips = got.argmax(1) != want.argmax(1)
+    assert np.all(margin[flips] <= 2 * REF_MODE_REL_TOL * np.abs(want).max()), margin[flips]
+    assert agree >= 0.995
 
 
 def test_dynamic_linear_exact_on_same_input(sd):
