@@ -98,6 +98,8 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
   }
   // D[feature][row]: lane (l32 = row, hi) holds features 8g + 4hi + e
   const int l32 = lane & 31, hi = lane >> 5;
+  // plain stores: write-through partials measured slower (split-K 15.3 -> 16.1 us
+  // with the finisher, profiles/r02_diag_write_through_ab.txt)
   int* pp = part + (long)s * m * n + col0 + 4 * hi;
   const int r = row0 + l32;
 #ifdef QCN_EXP_FC_NOSTORE   // diagnostic: no partial stores (results wrong by design)

@@ -169,9 +169,9 @@ QCN_DEV void stage_epik(const ConvEpi& ep, float* ek, int tid) {
 // rounds half-to-even and saturates to [0, 255] (probed exhaustively on gfx950,
 // tools/micro/cvt_probe.hip), and the fma / mul run as packed fp32 pairs:
 // 3 VALU per element instead of 7 (the epilogue is VALU-issue bound).
-template <int NQ, bool XORIN, bool FAST, bool D32 = false>
+template <int NQ, bool XORIN, bool FAST, bool D32 = false, bool GWT = false>
 QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
-                             int hi, uint8_t* orow) {
+                             int hi, uint8_t* orow, const uint8_t* wbase = nullptr, uint32_t woff = 0) {
   // accumulators already include the zero-point correction (acc_init_corr)
   uint32_t w[4];
   const float zpf = (float)ep.zp_y, lof = (float)ep.lo;
@@ -240,16 +240,19 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
 #pragma unroll
     for (int g = 0; g < 4; ++g) w[g] = xor80(w[g]);
   }
-  *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
+  if constexpr (GWT)   // orow unused: global destination wr + woff (write-through)
+    store_wt16(wt_rsrc(wbase), woff + co_base + 16 * hi, make_uint4(w[0], w[1], w[2], w[3]));
+  else
+    *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 QCN_DEV bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
 
-template <int NQ, bool XORIN = false, bool D32 = false>
+template <int NQ, bool XORIN = false, bool D32 = false, bool GWT = false>
 QCN_DEV void epilogue_tile_kf(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
-                              int hi, uint8_t* orow) {
-  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true, D32>(accs, K, ep, co_base, hi, orow);
-  else epilogue_tile_k<NQ, XORIN, false, D32>(accs, K, ep, co_base, hi, orow);
+                              int hi, uint8_t* orow, const uint8_t* wbase = nullptr, uint32_t woff = 0) {
+  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
+  else epilogue_tile_k<NQ, XORIN, false, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
 }
 
 template <int NQ, bool XORIN = false>
@@ -280,11 +283,12 @@ template <int COUT, int OS, int NT>
 QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid) {
   constexpr int CPR = COUT / 16;
   const int total = opx * CPR;
+  const wt_rsrc_t wr = wt_rsrc(dst);   // the next launch reads it: write through
   for (int e = tid; e < total; e += NT) {
     const int row = e / CPR, ch = e % CPR;
     if (row < valid_px)
-      *reinterpret_cast<uint4*>(dst + (long)row * COUT + ch * 16) =
-          *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16);
+      store_wt16(wr, (uint32_t)(row * COUT + ch * 16),
+                 *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16));
   }
 }
 
@@ -488,12 +492,13 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
     if constexpr (IMGS >= 1 && C::OPX % OPI == 0) {
       constexpr int CC = COUT / 32;
       const int n0 = (int)(out0 / OPI);
+      const wt_rsrc_t wr = wt_rsrc(y + (long)n0 * 32);   // offsets < 2^31: nimg * 4096 checked at launch
       for (int e = tid; e < OPI * CC * IMGS * 2; e += C::NT) {
         const int half = e & 1, img = (e >> 1) % IMGS, pc = (e >> 1) / IMGS;
         const int p = pc / CC, cc = pc % CC;
         if (n0 + img < nimg)
-          *reinterpret_cast<uint4*>(y + ((long)(p * CC + cc) * nimg + n0 + img) * 32 + half * 16) =
-              *reinterpret_cast<const uint4*>(lout + (img * OPI + p) * C::OS + cc * 32 + half * 16);
+          store_wt16(wr, (uint32_t)(((p * CC + cc) * nimg + img) * 32 + half * 16),
+                     *reinterpret_cast<const uint4*>(lout + (img * OPI + p) * C::OS + cc * 32 + half * 16));
       }
     }
     return;
@@ -679,6 +684,12 @@ __global__ __launch_bounds__(CA::NT, CA::WI == 4 ? 1 : 2)
 void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                      const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                      const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+#ifdef QCN_STAMPS   // where each workgroup ran: HW_ID (CU, SE, slot) and XCC_ID
+  if (threadIdx.x == 0) {
+    qcn_stamps[(blockIdx.x + 16384) & 0xffff][0] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
+    qcn_stamps[(blockIdx.x + 16384) & 0xffff][1] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));
+  }
+#endif
   convpair_body<CA, CB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
@@ -1246,6 +1257,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     const int n = t >> 1, h = t & 1;
     const float* ek2 = reinterpret_cast<const float*>(lds + L::OFF_EPI2);
     uint8_t* dst = y + ((long)n * 256 + h * 128 + wave * 32 + l32) * 64;
+    const uint8_t* wbase = y + ((long)n * 256 + h * 128) * 64;   // write-through destination
+    const uint32_t woff = (uint32_t)((wave * 32 + l32) * 64);
 #ifdef QCN_EXP_NOEPI
     {  // keep every accumulator live (no DCE), skip the requant
       int x = 0;
@@ -1261,7 +1274,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #endif
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      epilogue_tile_kf<4>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi, dst);
+      epilogue_tile_kf<4, false, false, true>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi,
+                                              dst, wbase, woff);
   };
 
 #ifdef QCN_STAMPS
@@ -1544,6 +1558,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     epa.s1 = qdqa->s1; epa.z1 = qdqa->z1; epa.inv2 = qdqa->inv2; epa.z2 = qdqa->z2;
     xb_zp = qdqa->z2;
   }
+  if (kmajor && (long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
   ConvEpi epb{ub, vb, multb, corrb, y_zp, relub ? y_zp : 0, 0, 0.f, 0, 0.f, 0, kmajor ? 1 : 0};
   if (qdqb) {
     epb.qdq = 1;
@@ -1578,6 +1593,7 @@ int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, i
   if (pool && ((h & 1) || (w & 1))) return QCN_ERR_ARG;
   // whole images per workgroup: the 8x8 -> 4x4 and 8x8 layers of the net
   if (!(h == 8 && w == 8 && cin % 64 == 0 && cout == 256)) return QCN_ERR_UNSUPPORTED;
+  if ((long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
   ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 1};
   return dispatch_conv(cin, cout, h, pool, x, nimg, x_zp, w_packed, ep, y, (hipStream_t)stream);
 }
