@@ -823,7 +823,7 @@ struct Conv12P {
   static constexpr int WRES = 9 * C::WBUF;                 // all conv2 weights
   // quantized fp32 input window: rows y0-2..y0+17, cols -2..33, one dword per
   // pixel (c0, c1, c2, 0) so conv1's im2col operand is plain aligned dwords
-  static constexpr int IN_R = 20, IN_C = 36;
+  static constexpr int IN_R = 20, IN_C = 40;   // cols -4 .. 35: interior 16-B aligned
   static constexpr int IN8 = IN_R * IN_C * 4;
   static constexpr int OFF_W = 2 * PATCH;
   static constexpr int OFF_IN = OFF_W + WRES;              // 2 x quantized input window
@@ -920,7 +920,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   uint8_t* in8_1 = lds + L::OFF_IN + L::IN8;
 
   float4 xraw[3];
-  int xrow_ok = 0;
   const uint32_t padw = xor80(splat_u8(x2_zp));
   const uint4 pad4 = make_uint4(padw, padw, padw, padw);
   for (int e = tid; e < 2 * C::PROWS * 8; e += 512) {
@@ -957,6 +956,15 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
           w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4));
     }
 #endif
+    // the input windows' constant zero-point border (both buffers)
+    const uint32_t in_pad = xor80(splat_u8(in_zp)) & 0x00ffffffu;
+    for (int e = tid; e < 2 * L::IN_R * L::IN_C; e += 512) {
+      const int b = e / (L::IN_R * L::IN_C), rc = e % (L::IN_R * L::IN_C);
+      const int rr = rc / L::IN_C, cc = rc % L::IN_C;
+      const bool pad_row = b == 0 ? rr < 2 : rr >= 18;
+      if (pad_row || cc < 4 || cc >= 36)
+        reinterpret_cast<uint32_t*>(lds + L::OFF_IN + b * L::IN8)[rc] = in_pad;
+    }
     if (!producer) stage_epik<64, 256>(ep1, reinterpret_cast<float*>(lds + L::OFF_EPI1), tid);
     if (!producer) stage_epik<64, 256>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
     if (tid < 16)
@@ -986,14 +994,19 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       }
     }
   };
-  // Window staging, vectorised: producer thread pt < 180 owns window row
-  // rr = pt / 9 and columns 4g-2 .. 4g+1 (g = pt % 9) of all three channels:
-  // three 16-B loads (8-B aligned: dword-aligned is enough) and one 12-byte
-  // [col][c] run in LDS.  Out-of-image rows/columns quantize to in_zp.
-  // stage_load only issues the loads (raw float4s stay in registers, their
-  // latency hidden behind conv1_tile); stage_store selects, quantizes, writes.
+  // Window staging: the fp32 NCHW input rows of tile t, quantized (aten
+  // quantize_per_tensor) to one s8 dword (c0, c1, c2, 0) per pixel.  Window
+  // row rr is input row y0 - 2 + rr, window column cc is input column cc - 4.
+  // Only the image interior changes from tile to tile: the two rows outside
+  // the image (rows 0-1 of a top half, 18-19 of a bottom half — each half has
+  // its own buffer) and the side columns are zero points written once.
+  // Producer thread pt < 144 (waves 5-7) owns window row rr0 + pt / 8 and
+  // input columns 4g .. 4g + 3 (g = pt % 8): three aligned 16-B loads, 12
+  // values at 4 VALU each (mul, rndne, + zp, saturating v_cvt_pk_u8_f32), one
+  // ds_write_b128.  stage_load only issues the loads (their latency hides
+  // behind conv1_tile); stage_store quantizes and writes.
   // The window index math depends only on the thread id; laundering it
-  // through an empty asm per use keeps LICM from hoisting ~40 loop-invariant
+  // through an empty asm per use keeps LICM from hoisting loop-invariant
   // values out of the tile loop (they were spilled: the consumer's MFMA state
   // shares the register budget).
   auto fresh_ptid = [&]() {
@@ -1005,50 +1018,32 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     if (ptid < 0) return;   // wave 4 (whole wave): no window share
     const int n = t >> 1, y0 = (t & 1) * 16;
     const int pt = fresh_ptid();
-    const int rr = pt / 9, g = pt % 9;
-    const int iy = y0 - 2 + rr, c0 = 4 * g - 2;
-    const bool row_ok = pt >= 0 && pt < 180 && iy >= 0 && iy < 32;
-    xrow_ok = row_ok;
-    // columns c0..c0+3 lie in [0, 32) except for g = 0 (c0 = -2) and g = 8 (c0 = 30):
-    // load from a clamped in-row start, select per element at store time
-    const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
-    // unconditional loads (a clamped, valid row when outside): a divergent
-    // load made the compiler wait for it on the spot
-    const int iyc = iy < 0 ? 0 : (iy > 31 ? 31 : iy);
+    const int r = pt < 144 ? pt >> 3 : 0, g = pt & 7;
+    const int iy = y0 + (y0 == 0 ? 0 : -2) + r;   // rows 0..17 of the top half, 14..31 of the bottom
     const int nc = n < nimg ? n : nimg - 1;
 #pragma unroll
     for (int c = 0; c < 3; ++c)
-      xraw[c] = *reinterpret_cast<const float4*>(x + (((long)nc * 3 + c) * 32 + iyc) * 32 + cl);
+      xraw[c] = *reinterpret_cast<const float4*>(x + (((long)nc * 3 + c) * 32 + iy) * 32 + 4 * g);
   };
-  auto stage_store = [&](uint8_t* in8) {  // quantize (aten quantize_per_tensor) -> s8
+  auto stage_store = [&](uint8_t* in8, int half) {
     const int pt = fresh_ptid();
-    if (pt >= 0 && pt < 180) {
-      const int rr = pt / 9, g = pt % 9;
-      const int c0 = 4 * g - 2;
-      const int cl = c0 < 0 ? 0 : (c0 > 28 ? 28 : c0);
+    if (pt >= 0 && pt < 144) {
+      const int rr = (half ? 0 : 2) + (pt >> 3), g = pt & 7;
+      const float zpf = (float)in_zp;
       uint32_t wd[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int col = c0 + e;          // wanted column
-        const int idx = col - cl;        // its position in the loaded 4 (if inside)
-        const bool ok = xrow_ok && col >= 0 && col < 32;
         uint32_t d = 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          const float4 v = xraw[c];
-          const float xv = (idx == 0) ? v.x : (idx == 1) ? v.y : (idx == 2) ? v.z : v.w;
-          int q = in_zp;
-          if (ok) {
-            float t = xv * in_inv;
-            t = fminf(fmaxf(t, -1.0e9f), 1.0e9f);
-            q = (int)__builtin_rintf(t) + in_zp;
-            q = q < 0 ? 0 : (q > 255 ? 255 : q);
-          }
-          d |= (uint32_t)((q ^ 0x80) & 0xff) << (8 * c);
+          const float xv = e == 0 ? xraw[c].x : e == 1 ? xraw[c].y : e == 2 ? xraw[c].z : xraw[c].w;
+          // zp + rint(x / s), saturated to [0, 255]; rint(...) + zp is exact
+          // below 2^24 and saturates the same way above
+          d = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_rintf(xv * in_inv) + zpf, c, d);
         }
-        wd[e] = d;
+        wd[e] = d ^ 0x00808080u;
       }
-      *reinterpret_cast<uint4*>(in8 + (rr * L::IN_C + 4 * g) * 4) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+      *reinterpret_cast<uint4*>(in8 + (rr * L::IN_C + 4 + 4 * g) * 4) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
   };
   auto fresh = [](int v) {  // see fresh_ptid
@@ -1103,7 +1098,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     // low lanes carry taps (0,0) (0,1) (0,2) (1,0) with tap (2,2)'s channel c
     // in the pad byte of tap (0,c) (v_perm), high lanes (1,1) (1,2) (2,0) (2,1)
     auto bop = [&](int tr, v4i& b0) {
-      const int* r0 = in32 + (tr + 0) * L::IN_C + l32 + 1;   // input cols l32-1 .. l32+1
+      const int* r0 = in32 + (tr + 0) * L::IN_C + l32 + 3;   // input cols l32-1 .. l32+1
       const int* r1 = r0 + L::IN_C;
       const int* r2 = r1 + L::IN_C;
       if (hi == 0) {
@@ -1284,7 +1279,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #endif
   if (producer && T > 0) stage_load(tile_of(0));
   setup();
-  if (producer && T > 0) stage_store(in8_0);
+  if (producer && T > 0) stage_store(in8_0, 0);
 #ifndef QCN_EXP_SYNCW
   if (!producer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own weight DMA landed
 #endif
@@ -1326,7 +1321,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       const unsigned long long tb_ = __builtin_amdgcn_s_memtime();
       pb_ += tb_ - ta_;
 #endif
-      if (j + 1 < T) stage_store(((j + 1) & 1) ? in8_1 : in8_0);
+      if (j + 1 < T) stage_store(((j + 1) & 1) ? in8_1 : in8_0, (j + 1) & 1);
 #endif
     } else if (j >= 1) {
 #ifndef QCN_EXP_NOCONS
