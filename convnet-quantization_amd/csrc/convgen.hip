@@ -263,12 +263,14 @@ __global__ void stem_pack_kernel(const float* __restrict__ x, int n, int h, int 
   o[1] = make_uint4(wd[4], wd[5], wd[6], wd[7]);
 }
 
-// Global average pool + the classifier's QuantStub: per (image, channel)
-// mean = fp32(sum_q - hw*zp) * fp32(s_x / hw), then quantize_per_tensor.
-// The integer sum is exact; the two fp32 roundings are the whole definition
-// (oracle/qref.py avgpool_q restates it).  4 channels per thread.
+// Global average pool on u8 NHWC, quantization parameters kept (torch's
+// quantized adaptive_avg_pool2d to 1x1, what a static-int8 ResNet runs before
+// its fc): per (image, channel) acc = sum_q - hw * zp (exact), then
+// q = clamp(zp + rne(fp32(acc) * fp32(1 / hw)), 0, 255) — probed bit-exact
+// against torch 2.10 (fbgemm) at 2x2 and 7x7 with ties (oracle qref.avgpool_q).
+// 4 channels per thread.
 __global__ void avgpool_kernel(const uint8_t* __restrict__ x, int n, int hw, int c, int zp,
-                               float k, float inv_o, int zo, uint8_t* __restrict__ y) {
+                               float inv_hw, uint8_t* __restrict__ y) {
   const int c4 = c / 4;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long)n * c4) return;
@@ -281,14 +283,12 @@ __global__ void avgpool_kernel(const uint8_t* __restrict__ x, int n, int hw, int
     s0 += q & 0xff; s1 += (q >> 8) & 0xff; s2 += (q >> 16) & 0xff; s3 += q >> 24;
   }
   const int sums[4] = {s0, s1, s2, s3};
+  const float zpf = (float)zp;
   uint32_t o = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float m = (float)(sums[i] - hw * zp) * k;
-    const float t = fminf(fmaxf(m * inv_o, -1.0e9f), 1.0e9f);
-    int q = (int)__builtin_rintf(t) + zo;
-    q = q < 0 ? 0 : (q > 255 ? 255 : q);
-    o |= (uint32_t)q << (8 * i);
+    const float t = __builtin_rintf((float)(sums[i] - hw * zp) * inv_hw) + zpf;   // exact integer
+    o = __builtin_amdgcn_cvt_pk_u8_f32(t, i, o);                                    // clamp [0, 255]
   }
   *reinterpret_cast<uint32_t*>(y + img * c + cb * 4) = o;
 }
@@ -366,16 +366,13 @@ int qcn_stem_pack_f32_nchw(const float* x, int nimg, int h, int w, float scale, 
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, float x_scale, int x_zp,
-                        float s_out, int z_out, uint8_t* y, void* stream) {
-  if (!x || !y || nimg <= 0 || hw <= 0 || c <= 0 || !(x_scale > 0.f) || !(s_out > 0.f) ||
-      x_zp < 0 || x_zp > 255 || z_out < 0 || z_out > 255)
-    return QCN_ERR_ARG;
+int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, int x_zp, uint8_t* y,
+                        void* stream) {
+  if (!x || !y || nimg <= 0 || hw <= 0 || c <= 0 || x_zp < 0 || x_zp > 255) return QCN_ERR_ARG;
   if (c % 4 != 0 || hw > (1 << 16)) return QCN_ERR_UNSUPPORTED;
   const long total = (long)nimg * (c / 4);
-  const float k = x_scale / (float)hw;
   hipLaunchKernelGGL(qcn::avgpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, x, nimg, hw, c, x_zp, k, 1.0f / s_out, z_out, y);
+                     (hipStream_t)stream, x, nimg, hw, c, x_zp, 1.0f / (float)hw, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

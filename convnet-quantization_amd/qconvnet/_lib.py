@@ -73,7 +73,7 @@ SIGNATURES = {
     "qcn_add_relu_u8": (i32, [vp, f32, i32, vp, f32, i32, i64, f32, i32, i32, vp, vp]),
     "qcn_maxpool3x3s2_u8_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_stem_pack_f32_nchw": (i32, [vp, i32, i32, i32, f32, i32, vp, vp]),
-    "qcn_avgpool_u8_nhwc": (i32, [vp, i32, i32, i32, f32, i32, f32, i32, vp, vp]),
+    "qcn_avgpool_u8_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_linear_dynamic_workspace_size": (i64, [i32, i32]),
     "qcn_linear_dynamic_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp]),
     "qcn_linear_dynamic_range_f32": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp, vp, vp,

@@ -417,11 +417,12 @@ def stem_pack(x, scale, zp, out=None):
     return out
 
 
-def avgpool(x, x_scale, x_zp, s_out, z_out, out=None):
+def avgpool(x, x_zp, out=None):
+    """Global average pool of u8 NHWC [n,h,w,c] -> [n,c], qparams kept
+    (torch's quantized adaptive_avg_pool2d)."""
     _need(x, torch.uint8, "avgpool.x")
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty((n, c), dtype=torch.uint8, device=x.device)
-    check(lib().qcn_avgpool_u8_nhwc(_ptr(x), n, h * w, c, float(x_scale), int(x_zp), float(s_out),
-                                    int(z_out), _ptr(out), _stream()), "avgpool")
+    check(lib().qcn_avgpool_u8_nhwc(_ptr(x), n, h * w, c, int(x_zp), _ptr(out), _stream()), "avgpool")
     return out

@@ -15,7 +15,7 @@ Device pipeline per forward (all u8 NHWC, every launch a hand-written HIP
 kernel on the current stream, capturable into a HIP graph):
   stem_pack (QuantStub + 7-tap row im2col) -> conv 7x1 (the 7x7/2 stem) ->
   maxpool 3x3/2 -> 16 x [conv1x1+ReLU -> conv3x3(/2)+ReLU -> conv1x1
-  (-> downsample conv1x1(/2)) -> add+ReLU] -> avgpool+quantize -> fc (fp32 logits)
+  (-> downsample conv1x1(/2)) -> add+ReLU] -> avgpool (u8, qparams kept) -> fc (fp32 logits)
 """
 from __future__ import annotations
 
@@ -68,10 +68,13 @@ def fold_state_dict(sd):
 
 
 # ============================================================ calibration
-def calibrate(folded, batches, device="cuda"):
+def calibrate(folded, batches, device="cpu"):
     """fp32 forward of the folded net recording every observer's range:
     x, stem (post-ReLU), per block c1/c2 (post-ReLU), c3 and ds (pre-add),
-    out (post add+ReLU), pool (avgpool output), fc."""
+    out (post add+ReLU), fc.  On the CPU (the default) the ranges are those
+    torch.ao's observers record on the same host (same fp32 ops, same folded
+    weights) and do not change from run to run; device="cuda" uses the HIP
+    min/max observer behind MIOpen's fp32 convs (faster, not bit-stable)."""
     dev = torch.device(device)
 
     def t(a):
@@ -80,7 +83,7 @@ def calibrate(folded, batches, device="cuda"):
     stem = [t(a) for a in folded["stem"]]
     blocks = [{k: (t(v[0]), t(v[1]), v[2], v[3]) for k, v in b.items()} for b in folded["blocks"]]
     fc = [t(a) for a in folded["fc"]]
-    rng = {"x": _Range(dev), "stem": _Range(dev), "pool": _Range(dev), "fc": _Range(dev)}
+    rng = {"x": _Range(dev), "stem": _Range(dev), "fc": _Range(dev)}
     for i, b in enumerate(blocks):
         for k in list(b) + ["out"]:
             rng[f"b{i}.{k}"] = _Range(dev)
@@ -107,8 +110,7 @@ def calibrate(folded, batches, device="cuda"):
                     rng[f"b{i}.ds"](idn)
                 x = F.relu(y + idn)
                 rng[f"b{i}.out"](x)
-            x = x.mean((2, 3))
-            rng["pool"](x)
+            x = x.mean((2, 3))   # (the int8 net pools the quantized map, qparams kept)
             x = F.linear(x, fc[0], fc[1])
             rng["fc"](x)
     return {k: r.values() for k, r in rng.items()}
@@ -139,19 +141,22 @@ def build_spec(folded, ranges, per_channel=True):
         e["out"] = Q.qparams_affine(*ranges[f"b{i}.out"])
         spec["blocks"].append(e)
         s_x, z_x = e["out"]
-    spec["pool"] = Q.qparams_affine(*ranges["pool"])
+    # avgpool runs on the quantized map and keeps its qparams (torch.ao's
+    # quantized adaptive_avg_pool2d), so the fc's input qparams are the last
+    # block's output qparams
     w, b = folded["fc"]
     s_w = _weight_scale(w, per_channel)
     s_y, z_y = Q.qparams_affine(*ranges["fc"])
     spec["fc"] = dict(w=Q.quantize_weight(w, s_w), b=np.asarray(b, F32), s_w=s_w,
-                      s_x=spec["pool"][0], z_x=spec["pool"][1], s_y=s_y, z_y=z_y, relu=False)
+                      s_x=s_x, z_x=z_x, s_y=s_y, z_y=z_y, relu=False)
     return spec
 
 
-def quantize_resnet(model, calib_batches, device="cuda", per_channel=True):
-    """fp32 ResNet (models.resnet / torchvision layout) -> QuantizedResNet."""
+def quantize_resnet(model, calib_batches, device="cuda", per_channel=True, calibration_device="cpu"):
+    """fp32 ResNet (models.resnet / torchvision layout) -> QuantizedResNet on
+    `device`; calibration runs on `calibration_device` (CPU: deterministic)."""
     folded = fold_state_dict(model.state_dict())
-    ranges = calibrate(folded, calib_batches, device)
+    ranges = calibrate(folded, calib_batches, calibration_device)
     return QuantizedResNet(build_spec(folded, ranges, per_channel), device)
 
 
@@ -266,8 +271,7 @@ class QuantizedResNet:
             if keep:
                 inter[f"block{i}"] = q
         last = sp["blocks"][-1]["out"] if sp["blocks"] else (sp["stem"]["s_y"], sp["stem"]["z_y"])
-        sp_, zp_ = sp["pool"]
-        q = ops.avgpool(q, last[0], last[1], sp_, zp_)
+        q = ops.avgpool(q, last[1])   # qparams kept: the fc reads `last`'s qparams
         mark("avgpool")
         if keep:
             inter["pool"] = q

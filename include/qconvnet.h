@@ -246,10 +246,12 @@ int qcn_maxpool3x3s2_u8_nhwc(const uint8_t* x, int nimg, int h, int w, int c, ui
  * zero point outside the image and in bytes 21..31.  ow = (w-1)/2 + 1. */
 int qcn_stem_pack_f32_nchw(const float* x, int nimg, int h, int w, float scale, int zp, uint8_t* y,
                            void* stream);
-/* AdaptiveAvgPool2d(1) + the fc's QuantStub: y[n][c] =
- * quantize(fp32(sum_q - hw*x_zp) * fp32(x_scale/hw), s_out, z_out). */
-int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, float x_scale, int x_zp,
-                        float s_out, int z_out, uint8_t* y, void* stream);
+/* AdaptiveAvgPool2d(1) on u8 NHWC [nimg][hw][c] -> [nimg][c], quantization
+ * parameters kept (torch's quantized adaptive_avg_pool2d, the avgpool of a
+ * static-int8 ResNet ahead of its fc): y = clamp(x_zp + rne(fp32(sum_q -
+ * hw*x_zp) * fp32(1/hw)), 0, 255).  c % 4 == 0. */
+int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, int x_zp, uint8_t* y,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -449,11 +449,113 @@ def gen_resnet_ops(rng):
     np.savez_compressed(os.path.join(OUT, "ops_resnet.npz"), **cases)
 
 
+def _resnet_spec_from_torchao(q):
+    """The oracle's ResNet spec (qref.resnet_int8_forward's format, the same
+    as qconvnet.resnet.build_spec's) read out of a converted ResNetRef."""
+    def layer(m, s_x, z_x, relu, stride, pad):
+        wq = m.weight()
+        s_w = (F32(wq.q_scale()) if wq.qscheme() in (torch.per_tensor_affine, torch.per_tensor_symmetric)
+               else wq.q_per_channel_scales().numpy().astype(F32))
+        return dict(w=wq.int_repr().numpy(), b=m.bias().detach().numpy().astype(F32), s_w=s_w,
+                    s_x=F32(s_x), z_x=int(z_x), s_y=F32(m.scale), z_y=int(m.zero_point), relu=relu,
+                    stride=(stride, stride), pad=(pad, pad))
+    spec = {"per_channel": True, "blocks": [],
+            "in": (F32(q.quant.scale.item()), int(q.quant.zero_point.item()))}
+    spec["stem"] = layer(q.conv1, *spec["in"], True, 2, 3)
+    s_x, z_x = spec["stem"]["s_y"], spec["stem"]["z_y"]
+    for li in range(1, 5):
+        for blk in getattr(q, f"layer{li}"):
+            st = blk.conv2.stride[0]
+            e = {"c1": layer(blk.conv1, s_x, z_x, True, 1, 0)}
+            e["c2"] = layer(blk.conv2, e["c1"]["s_y"], e["c1"]["z_y"], True, st, 1)
+            e["c3"] = layer(blk.conv3, e["c2"]["s_y"], e["c2"]["z_y"], False, 1, 0)
+            e["ds"] = (layer(blk.downsample[0], s_x, z_x, False, blk.downsample[0].stride[0], 0)
+                       if blk.downsample is not None else None)
+            e["out"] = (F32(blk.q_out.scale.item()), int(blk.q_out.zero_point.item()))
+            spec["blocks"].append(e)
+            s_x, z_x = e["out"]
+    fc = q.fc
+    wq = fc.weight()
+    spec["fc"] = dict(w=wq.int_repr().numpy(), b=fc.bias().detach().numpy().astype(F32),
+                      s_w=wq.q_per_channel_scales().numpy().astype(F32), s_x=s_x, z_x=z_x,
+                      s_y=F32(fc.scale), z_y=int(fc.zero_point), relu=False)
+    return spec
+
+
+def gen_resnet_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
+    """SURVEY §8(f)2 whole-network pin: a 1-1-1-1 bottleneck ResNet at 64x64
+    as torch.ao eager static int8 (fbgemm; per-channel MinMax weights, MinMax
+    u8 activations, float-domain residual join, quantized max-pool /
+    avg-pool / fc), calibrated on the CPU.  Stores what regenerates the model
+    (BN running statistics; weights come from torch_ref.resnet_state_dict),
+    every qparam, int8-weight hashes, every block's u8 output by hash, the
+    pooled u8 features and the logits; asserts the numpy oracle
+    (qref.resnet_int8_forward) reproduces it bit for bit."""
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    imnet = dict(mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), hw=hw)
+    fp = tr.ResNetRef(layers, num_classes)
+    fp.load_state_dict(tr.resnet_state_dict(fp, 0))
+    tr.recalibrate_bn(fp, torch.from_numpy(tr.synthetic_images(16, 3, **imnet)))
+    calib = tr.synthetic_images(8, 4, **imnet)
+    q = tr.build_resnet_static_int8_cpu(fp, [torch.from_numpy(calib)])
+    x = tr.synthetic_images(n, 5, **imnet)
+    outs, order = {}, []
+    hooks = [q.maxpool.register_forward_hook(lambda m, a, o: outs.__setitem__("stem", o)),
+             q.avgpool.register_forward_hook(lambda m, a, o: outs.__setitem__("pool", o)),
+             q.fc.register_forward_hook(lambda m, a, o: outs.__setitem__("fc", o))]
+    for li in range(1, 5):
+        for bi, blk in enumerate(getattr(q, f"layer{li}")):
+            k = f"block{len(order)}"
+            order.append(k)
+            hooks.append(blk.register_forward_hook(lambda m, a, o, k=k: outs.__setitem__(k, o)))
+    with torch.no_grad():
+        logits = q(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    spec = _resnet_spec_from_torchao(q)
+    mine, inter = qref.resnet_int8_forward(x, spec, keep=True)
+    nhwc = lambda t: t.int_repr().permute(0, 2, 3, 1).contiguous().numpy()  # noqa: E731
+    assert (inter["stem"] == nhwc(outs["stem"])).all(), "stem"
+    for k in order:
+        assert (inter[k] == nhwc(outs[k])).all(), k
+    pool = outs["pool"].int_repr().reshape(n, -1).numpy()
+    assert (inter["pool"] == pool).all(), "avgpool"
+    assert (mine == logits).all(), "logits"
+    rec = {"layers": np.asarray(layers, np.int64), "hw": np.int64(hw), "batch": np.int64(n),
+           "num_classes": np.int64(num_classes), "x_sha": sha(x), "calib_sha": sha(calib),
+           "logits": logits, "q_logits": outs["fc"].int_repr().numpy(), "pool": pool,
+           "stem_sha": sha(inter["stem"])}
+    for k in order:
+        rec[f"{k}_sha"] = sha(inter[k])
+    for k, v in fp.state_dict().items():   # BN running statistics (the recalibrated state)
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            rec["sd." + k] = v.numpy()
+    rec["in_q"] = np.asarray(spec["in"][0], F32), np.int64(spec["in"][1])
+    rec["in_scale"], rec["in_zp"] = F32(spec["in"][0]), np.int64(spec["in"][1])
+    def put(name, e):
+        rec[name + ".s_y"], rec[name + ".z_y"] = F32(e["s_y"]), np.int64(e["z_y"])
+        rec[name + ".w_sha"] = sha(e["w"])
+    put("stem", spec["stem"])
+    for i, e in enumerate(spec["blocks"]):
+        for k in ("c1", "c2", "c3", "ds"):
+            if e[k] is not None:
+                put(f"b{i}.{k}", e[k])
+        rec[f"b{i}.out_scale"], rec[f"b{i}.out_zp"] = F32(e["out"][0]), np.int64(e["out"][1])
+    put("fc", spec["fc"])
+    del rec["in_q"]
+    np.savez_compressed(os.path.join(OUT, "net_resnet_int8.npz"), **rec)
+    return rec
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.backends.quantized.engine = "fbgemm"
     if sys.argv[1:] == ["resnet"]:   # only the §8(f)2 vectors
         gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
+        return
+    if sys.argv[1:] == ["resnet_net"]:   # only the §8(f)2 whole-net vectors
+        gen_resnet_net()
         return
     if sys.argv[1:] == ["headline"]:   # only the batch-1024 / batch-256 whole-net vectors
         gen_net_headline(per_channel=False)
@@ -472,6 +574,7 @@ def main():
     gen_net_headline(per_channel=True)
     gen_qdq_config2()
     gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
+    gen_resnet_net()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

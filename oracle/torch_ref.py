@@ -240,3 +240,122 @@ def build_qdq_cpu(fp32, calib_batches, per_channel=False):
             net(xb)
     tq.convert(net, inplace=True)
     return net.eval()
+
+
+# -------------------------------------------------------------------------- ResNet
+class BottleneckRef(nn.Module):
+    """torchvision Bottleneck (v1.5: stride on the 3x3), the block the
+    reference wraps as CustomQuantizedBottleneck
+    (/root/reference/models/custom_quantization_model.py:60-102); one ReLU
+    module per use so torch.ao eager fusion can pair each conv with its own."""
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu1 = nn.ReLU()
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.relu2 = nn.ReLU()
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.downsample = downsample
+        # static-int8 hand-off of the float-domain residual join (:94-101):
+        # dequantize both operands, add in fp32, ReLU, quantize
+        self.dq_out, self.dq_id, self.q_out = tq.DeQuantStub(), tq.DeQuantStub(), tq.QuantStub()
+
+    def forward(self, x):
+        out = self.relu1(self.bn1(self.conv1(x)))
+        out = self.relu2(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        idn = self.downsample(x) if self.downsample is not None else x
+        return self.q_out(F.relu(self.dq_out(out) + self.dq_id(idn)))
+
+
+class ResNetRef(nn.Module):
+    """torchvision ResNet layout (same state-dict keys as models.resnet /
+    torchvision.models.resnet50), quantization stubs at the net's ends."""
+
+    def __init__(self, layers=(1, 1, 1, 1), num_classes=10, base=64):
+        super().__init__()
+        self.quant, self.dequant = tq.QuantStub(), tq.DeQuantStub()
+        self.inplanes = base
+        self.conv1 = nn.Conv2d(3, base, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(base)
+        self.relu = nn.ReLU()
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        for i, n in enumerate(layers, start=1):
+            planes, stride = base * 2 ** (i - 1), 1 if i == 1 else 2
+            ds = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                               nn.BatchNorm2d(planes * 4))
+            blocks = [BottleneckRef(self.inplanes, planes, stride, ds)]
+            self.inplanes = planes * 4
+            blocks += [BottleneckRef(self.inplanes, planes) for _ in range(1, n)]
+            setattr(self, f"layer{i}", nn.Sequential(*blocks))
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(base * 8 * 4, num_classes)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(self.quant(x)))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.dequant(self.fc(torch.flatten(self.avgpool(x), 1)))
+
+
+def resnet_state_dict(model, seed=0):
+    """Version-stable synthetic weights for a ResNetRef / models.resnet net:
+    Kaiming-normal(fan_out) convs, uniform(0.5, 1.5) BN gamma, 0.1 N(0,1) BN
+    beta (as models.resnet.synthetic_resnet spreads them), N(0, 0.01) fc,
+    zero fc bias, from numpy PCG64 in state-dict order."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sd = {}
+    for k, v in model.state_dict().items():
+        shape = tuple(v.shape)
+        if k.endswith("num_batches_tracked"):
+            sd[k] = torch.tensor(0, dtype=torch.long)
+            continue
+        if k.endswith("running_mean"):
+            a = np.zeros(shape, np.float32)
+        elif k.endswith("running_var"):
+            a = np.ones(shape, np.float32)
+        elif k.startswith("fc."):
+            a = (rng.standard_normal(shape) * 0.01).astype(np.float32) if k.endswith("weight") \
+                else np.zeros(shape, np.float32)
+        elif v.dim() == 4:   # conv
+            a = (rng.standard_normal(shape) * np.sqrt(2.0 / (shape[0] * shape[2] * shape[3]))).astype(np.float32)
+        elif k.endswith("weight"):   # BN gamma
+            a = (0.5 + rng.random(shape)).astype(np.float32)
+        else:   # BN beta
+            a = (0.1 * rng.standard_normal(shape)).astype(np.float32)
+        sd[k] = torch.from_numpy(a)
+    return sd
+
+
+def resnet_fuse_list(model):
+    fuse = [["conv1", "bn1", "relu"]]
+    for name, mod in model.named_modules():
+        if isinstance(mod, BottleneckRef):
+            fuse += [[f"{name}.conv1", f"{name}.bn1", f"{name}.relu1"],
+                     [f"{name}.conv2", f"{name}.bn2", f"{name}.relu2"],
+                     [f"{name}.conv3", f"{name}.bn3"]]
+            if mod.downsample is not None:
+                fuse.append([f"{name}.downsample.0", f"{name}.downsample.1"])
+    return fuse
+
+
+def build_resnet_static_int8_cpu(fp32, calib_batches, per_channel=True):
+    """torch.ao eager static int8 (fbgemm) of a ResNetRef: Conv-BN(-ReLU)
+    fused as /root/reference/models/custom_quantization_model.py:264-298 fuses
+    them, MinMax observers (per-channel symmetric s8 weights, per-tensor
+    affine u8 activations), float-domain residual join, quantized
+    max-pool / adaptive avg-pool / Linear."""
+    torch.backends.quantized.engine = "fbgemm"
+    net = copy.deepcopy(fp32).eval()
+    net = tq.fuse_modules(net, resnet_fuse_list(net), inplace=False)
+    net.qconfig = static_qconfig(per_channel)
+    tq.prepare(net, inplace=True)
+    with torch.no_grad():
+        for xb in calib_batches:
+            net(xb)
+    tq.convert(net, inplace=True)
+    return net.eval()

@@ -1,8 +1,10 @@
 """GPU parity for SURVEY §8(f)2 (ResNet-style bottleneck blocks, config 5):
 the general int8 conv, residual join, maxpool 3x3/2, stem packing and average
 pool kernels (through the C ABI) against the torch.ao golden vectors and the
-numpy oracle, then whole networks (a 1-block-per-stage ResNet at 64x64 and the
-full ResNet-50 at 224x224) bit-exact against oracle.qref.resnet_int8_forward."""
+numpy oracle, then whole networks: the 1-block-per-stage ResNet at 64x64
+bit-exact against torch.ao eager static int8 (tests/golden/net_resnet_int8.npz),
+and (on synthetic weights) the same net and the full ResNet-50 at 224x224
+bit-exact against oracle.qref.resnet_int8_forward."""
 import os
 
 import numpy as np
@@ -148,10 +150,15 @@ def test_stem_pack_and_stem_conv(dev, golden_dir):
 
 
 def test_avgpool(dev):
+    """Quantized global average pool (qparams kept) == the oracle, which is
+    pinned to torch's quantized adaptive_avg_pool2d (test_resnet_cpu fixture
+    test); 2x2 maps have exact .5 ties."""
     from qconvnet import ops
-    q = np.random.default_rng(7).integers(0, 256, (3, 7, 7, 2048)).astype(np.uint8)
-    out = ops.avgpool(torch.from_numpy(q).to(dev), 0.05, 11, 0.03, 0).cpu().numpy()
-    assert np.array_equal(out, qref.avgpool_q(q, 0.05, 11, 0.03, 0))
+    g = np.random.default_rng(7)
+    for shape, zp in (((3, 7, 7, 2048), 11), ((5, 2, 2, 2048), 0), ((2, 2, 2, 64), 200)):
+        q = g.integers(0, 256, shape).astype(np.uint8)
+        out = ops.avgpool(torch.from_numpy(q).to(dev), zp).cpu().numpy()
+        assert np.array_equal(out, qref.avgpool_q(q, zp)), shape
 
 
 def _net(dev, layers, hw, seed):
@@ -180,6 +187,26 @@ def test_resnet_bit_exact(dev, layers, hw, n):
     assert rel < 0.35, rel
 
 
+def test_resnet_equals_torchao_fixture(dev):
+    """§8(f)2 whole-net pin on the GPU: the 1-1-1-1 bottleneck ResNet at 64x64
+    with torch.ao's qparams (tests/golden/net_resnet_int8.npz) — stem, every
+    block's u8 output, pooled features and logits bit-exact to torch.ao eager
+    static int8 (fbgemm)."""
+    import resnetfix
+    from qconvnet.resnet import QuantizedResNet
+    z = resnetfix.load()
+    sp = resnetfix.spec(z)
+    assert resnetfix.check_weights(sp, z) == []
+    qm = QuantizedResNet(sp, dev)
+    logits, inter = qm.run(torch.from_numpy(resnetfix.images(z)).to(dev), keep=True)
+    torch.cuda.synchronize()
+    assert resnetfix.sha(inter["stem"].cpu().numpy()) == str(z["stem_sha"])
+    for i in range(len(sp["blocks"])):
+        assert resnetfix.sha(inter[f"block{i}"].cpu().numpy()) == str(z[f"block{i}_sha"]), i
+    assert np.array_equal(inter["pool"].cpu().numpy(), z["pool"])
+    assert np.array_equal(logits.cpu().numpy(), z["logits"])
+
+
 def test_custom_quantized_resnet50_wrapper(dev):
     """The models.custom_quantization_model drop-in builds the same executor."""
     from models.custom_quantization_model import CustomQuantizedResNet50
@@ -191,8 +218,8 @@ def test_custom_quantized_resnet50_wrapper(dev):
     x = synthetic_images(3, 6, 64)
     out = w(torch.from_numpy(x))
     assert out.shape == (3, 10) and out.device.type == "cpu"
-    # (MIOpen's fp32 calibration convs may pick different algorithms per call,
-    # so the wrapper is checked against the oracle on its own spec)
     ref, _ = qref.resnet_int8_forward(x, w.quantized_model.spec)
     assert np.array_equal(out.numpy(), ref)
-    assert isinstance(w.quantized_model, type(quantize_resnet(m, calib, dev)))
+    # calibration runs on the CPU by default: a second quantization is identical
+    again = quantize_resnet(m, calib, dev)
+    assert np.array_equal(again(torch.from_numpy(x)).numpy(), out.numpy())

@@ -59,3 +59,42 @@ def test_static_int8_spec_tracks_fp32():
         ref = m(torch.from_numpy(x)).numpy()
     assert np.abs(logits - ref).max() / np.abs(ref).max() < 0.3
     assert inter["block3"].shape == (4, 2, 2, 2048)
+
+
+def test_oracle_matches_torchao_resnet_fixture():
+    """§8(f)2 pin: torch.ao eager static int8 of a 1-1-1-1 bottleneck ResNet
+    at 64x64 (tests/golden/net_resnet_int8.npz) == the numpy oracle run on the
+    product's own folded / quantized weights: stem, every block, the pooled
+    features and the logits, bit for bit."""
+    import resnetfix
+    z = resnetfix.load()
+    sp = resnetfix.spec(z)
+    assert resnetfix.check_weights(sp, z) == []
+    logits, inter = qref.resnet_int8_forward(resnetfix.images(z), sp, keep=True)
+    assert resnetfix.sha(inter["stem"]) == str(z["stem_sha"])
+    for i in range(len(sp["blocks"])):
+        assert resnetfix.sha(inter[f"block{i}"]) == str(z[f"block{i}_sha"]), i
+    assert np.array_equal(inter["pool"], z["pool"])
+    assert np.array_equal(logits, z["logits"])
+
+
+def test_product_cpu_calibration_reproduces_torchao_qparams():
+    """The product's CPU calibration (qconvnet.resnet.calibrate, default device)
+    over the fixture's calibration images gives torch.ao's observer qparams
+    exactly (same fp32 ops on the same folded weights)."""
+    import resnetfix
+    from qconvnet.resnet import build_spec, calibrate, fold_state_dict
+    z = resnetfix.load()
+    folded = fold_state_dict(resnetfix.fp32_model(z).state_dict())
+    ranges = calibrate(folded, [torch.from_numpy(resnetfix.images(z, "calib"))])
+    sp = build_spec(folded, ranges, per_channel=True)
+    assert (np.float32(sp["in"][0]), sp["in"][1]) == (np.float32(z["in_scale"]), int(z["in_zp"]))
+    assert (sp["stem"]["s_y"], sp["stem"]["z_y"]) == (np.float32(z["stem.s_y"]), int(z["stem.z_y"]))
+    for i, e in enumerate(sp["blocks"]):
+        for k in ("c1", "c2", "c3", "ds"):
+            if e[k] is not None:
+                assert (e[k]["s_y"], e[k]["z_y"]) == (np.float32(z[f"b{i}.{k}.s_y"]),
+                                                      int(z[f"b{i}.{k}.z_y"])), (i, k)
+        assert (np.float32(e["out"][0]), e["out"][1]) == (np.float32(z[f"b{i}.out_scale"]),
+                                                          int(z[f"b{i}.out_zp"])), i
+    assert (sp["fc"]["s_y"], sp["fc"]["z_y"]) == (np.float32(z["fc.s_y"]), int(z["fc.z_y"]))
