@@ -80,13 +80,8 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
       const uint4 a = f0[buf][u], b = f1[buf][u];
       const v4i b0 = (v4i){(int)xor80(a.x), (int)xor80(a.y), (int)xor80(a.z), (int)xor80(a.w)};
       const v4i b1 = (v4i){(int)xor80(b.x), (int)xor80(b.y), (int)xor80(b.z), (int)xor80(b.w)};
-#ifndef QCN_EXP_FC_NOMFMA
       acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b0, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b1, acc1, 0, 0, 0);
-#else   // diagnostic: loads only (results wrong by design)
-      acc0[u] ^= fw[buf][u][0] ^ b0[1];
-      acc1[u] ^= fw[buf][u][2] ^ b1[3];
-#endif
     }
   };
   load(0, 0);
@@ -102,12 +97,6 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
   // with the finisher, profiles/r02_diag_write_through_ab.txt)
   int* pp = part + (long)s * m * n + col0 + 4 * hi;
   const int r = row0 + l32;
-#ifdef QCN_EXP_FC_NOSTORE   // diagnostic: no partial stores (results wrong by design)
-  int z = 0;
-#pragma unroll
-  for (int e = 0; e < 16; ++e) z ^= acc0[e] ^ acc1[e];
-  if (z != 0x12345678) return;
-#endif
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     *reinterpret_cast<int4*>(pp + (long)r * n + 8 * g) =

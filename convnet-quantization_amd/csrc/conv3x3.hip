@@ -187,18 +187,6 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
       if constexpr (NQ == 4) a[e] = max(max(a[e], accs[1][rg]), max(accs[2][rg], accs[3][rg]));
     }
     if constexpr (FAST) {
-#ifdef QCN_PK_REQ
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        const int rg = 4 * g + e;
-        const v2f af = {(float)a[e], (float)a[e + 1]};
-        const v2f t = __builtin_elementwise_fma((v2f){K.u[rg], K.u[rg + 1]},
-                                                (v2f){K.v[rg], K.v[rg + 1]}, af);
-        const v2f ab = t * (v2f){K.m[rg], K.m[rg + 1]};
-        wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.x, e, wd);
-        wd = __builtin_amdgcn_cvt_pk_u8_f32(ab.y, e + 1, wd);
-      }
-#else
       // scalar fma / mul (built with -fno-slp-vectorize so they stay scalar):
       // packed fp32 issues slower beside a partner wave's MFMAs
 #pragma unroll
@@ -208,7 +196,6 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
         f = f * K.m[rg];
         wd = __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
       }
-#endif
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -412,9 +399,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
       for (int g = 0; g < C::NG; ++g)
         if (dma && m == (2 * g + 1) * MPS / (2 * C::NG)) {
           __builtin_amdgcn_sched_barrier(0);
-#ifndef QCN_EXP_NODMA
           issue_g(dch, g);
-#endif
         }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -660,14 +645,8 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
       for (int j = 0; j < 4; ++j) {
         const int m = (wp * 4 + j) * 32 + l32;
         const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
-#if defined(QCN_EXP_NOEPIA)
-        if (acc[i][j][0] == 0x7fffffff) lds[CB::slot(seg, row + 1, col + 1)] = 1;
-#elif defined(QCN_EXP_PAIR_PERM)
-        epilogue_tile_kf<1, true>(&acc[i][j], K, epa, co_base, hi, lds + CB::slot(seg, row + 1, col + 1));
-#else
         epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
                                         lds + CB::slot(seg, row + 1, col + 1));
-#endif
       }
     }
   }
@@ -906,11 +885,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   const bool producer = wave >= 4;
   // window-staging thread id: producer waves 5-7 (0..191, 180 used).  Wave 4
   // computes the most conv1 rows of a top half (5 of 17), so it stages none
-#ifndef QCN_EXP_STAGE_W4
   const int ptid = tid - 320;
-#else
-  const int ptid = tid - 256;
-#endif
   // tile j of this workgroup: image t0 + (j / 2) * ts, top half then bottom
   // half (so every odd j reuses two conv1 rows from tile j - 1)
   auto tile_of = [&](int j) { return (t0 + (j >> 1) * ts) * 2 + (j & 1); };
@@ -935,7 +910,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     // constants of both layers, conv1's operand tables.  The weights go by
     // LDS-DMA (9 x 1 KB per consumer wave); the producer waves only load
     // their first input window meanwhile
-#ifndef QCN_EXP_SYNCW
     if (!producer) {
       const int wave_u = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
@@ -947,15 +921,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         glds16(w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), lds + L::OFF_W + p * 1024);
       }
     }
-#else
-    for (int e = tid; e < L::WRES / 16; e += 512) {
-      const int o = e * 16;
-      const int ch = o / C::WBUF, oc = o % C::WBUF;
-      const int r = oc >> 6, sl = (oc >> 4) & 3;
-      *reinterpret_cast<uint4*>(lds + L::OFF_W + o) = *reinterpret_cast<const uint4*>(
-          w2 + (long)ch * C::WBUF + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4));
-    }
-#endif
+
     // the input windows' constant zero-point border (both buffers)
     const uint32_t in_pad = xor80(splat_u8(in_zp)) & 0x00ffffffu;
     for (int e = tid; e < 2 * L::IN_R * L::IN_C; e += 512) {
@@ -1167,7 +1133,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
         // conv2 patch row
         auto requant_row = [&](const v16i (&acc)[2], int tr) {
           v2f t[2][8];
-#ifndef QCN_PK_REQ
           // scalar fma / mul (-fno-slp-vectorize keeps them scalar): packed fp32
           // beside another wave's MFMAs costs more issue than two scalar ops
           // (MI355X_MICROARCH 'price of one filler'); 53.5 -> 45.4 us here
@@ -1181,24 +1146,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
               f = f * (MODE == 1 ? sm : m[i][e]);
               t[i][e >> 1][e & 1] = f;
             }
-#else
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int pr = 0; pr < 8; ++pr)
-              t[i][pr] = (v2f){(float)acc[i][2 * pr], (float)acc[i][2 * pr + 1]};
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int pr = 0; pr < 8; ++pr)
-              t[i][pr] = __builtin_elementwise_fma((v2f){u[i][2 * pr], u[i][2 * pr + 1]}, (v2f){sv, sv},
-                                                   t[i][pr]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int pr = 0; pr < 8; ++pr)
-              t[i][pr] = t[i][pr] * (MODE == 1 ? (v2f){sm, sm} : (v2f){m[i][2 * pr], m[i][2 * pr + 1]});
-#endif
           uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
           // the lane's 4-channel groups 8g + 4hi go straight to their dwords in
           // the patch row (v_permlane32_swap costs ~25 cycles each,
@@ -1254,19 +1201,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     uint8_t* dst = y + ((long)n * 256 + h * 128 + wave * 32 + l32) * 64;
     const uint8_t* wbase = y + ((long)n * 256 + h * 128) * 64;   // write-through destination
     const uint32_t woff = (uint32_t)((wave * 32 + l32) * 64);
-#ifdef QCN_EXP_NOEPI
-    {  // keep every accumulator live (no DCE), skip the requant
-      int x = 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) x ^= acc[i][j][r];
-      if (x == 0x12345678) dst[0] = 1;
-      return;
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       epilogue_tile_kf<4, false, false, true>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi,
@@ -1280,9 +1214,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   if (producer && T > 0) stage_load(tile_of(0));
   setup();
   if (producer && T > 0) stage_store(in8_0, 0);
-#ifndef QCN_EXP_SYNCW
   if (!producer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own weight DMA landed
-#endif
   __syncthreads();
   // conv1 requant specialisation: v (and mult) identical across channels —
   // per-tensor weights give v = 1/aws, mult = aws/s_y; per-channel v = 1
@@ -1295,17 +1227,12 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
 #ifdef QCN_STAMPS
   const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
 #endif
-#ifndef QCN_EXP_NOSPLIT0
   constexpr bool SPLIT0 = true;
-#else
-  constexpr bool SPLIT0 = false;
-#endif
   for (int j = 0; j <= T; ++j) {
 #ifdef QCN_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
     if (producer) {
-#ifndef QCN_EXP_NOPROD
       if (j + 1 < T) stage_load(tile_of(j + 1));
 #ifdef QCN_STAMPS
       const unsigned long long ta_ = __builtin_amdgcn_s_memtime();
@@ -1322,11 +1249,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       pb_ += tb_ - ta_;
 #endif
       if (j + 1 < T) stage_store(((j + 1) & 1) ? in8_1 : in8_0, (j + 1) & 1);
-#endif
     } else if (j >= 1) {
-#ifndef QCN_EXP_NOCONS
       conv2_tile(tile_of(j - 1), ((j - 1) & 1) ? patch1 : patch0);
-#endif
     } else if (SPLIT0 && T > 0) {
       conv1_tile(tile_of(0), in8_0, patch0, nullptr, wave, 8);
       __builtin_amdgcn_s_setprio(0);

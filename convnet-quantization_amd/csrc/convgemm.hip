@@ -28,16 +28,12 @@ namespace qcn {
 // fp32(fp32(acc) + u*v) * mult for two channels (FBGEMM requant before the
 // rounding).  Scalar fma / mul (the build's -fno-slp-vectorize keeps them
 // scalar): packed fp32 issues slower beside a partner wave's MFMAs
-// (QCN_PK_REQ builds the packed form for A/B).
+// (profiles/r01_diag_scalar_vs_packed_requant.txt).
 QCN_DEV v2f requant2(int a0, int a1, v2f u, v2f v, v2f m) {
-#ifdef QCN_PK_REQ
-  return __builtin_elementwise_fma(u, v, (v2f){(float)a0, (float)a1}) * m;
-#else
   float x = __builtin_fmaf(u.x, v.x, (float)a0), y = __builtin_fmaf(u.y, v.y, (float)a1);
   x = x * m.x;
   y = y * m.y;
   return (v2f){x, y};
-#endif
 }
 
 

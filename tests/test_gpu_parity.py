@@ -349,8 +349,7 @@ def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
     assert torch.equal(y1, y1_ref)
     assert torch.equal(y2, y2_ref)
     assert torch.equal(y2f, y2f_ref)
-    # the workspace's row-block arrival counters stay valid across launches
-    # and batch sizes (the last workgroup of each row block writes the logits)
+    # the workspace is reusable across launches and batch sizes
     for mm in (m, 128, m, m):
         y2.zero_()
         y2f.zero_()
@@ -365,8 +364,8 @@ def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
 
 
 def test_classifier_head_repeated_full_batch(dev):
-    """The one-launch head at batch 1024 (256 workgroups, XCD-grouped row
-    blocks, arrival counters): 20 back-to-back launches on one workspace, each
+    """The classifier head at batch 1024 (split-K fc1 over 256 workgroups +
+    the per-row finisher): 20 back-to-back launches on one workspace, each
     bit-identical to fc1 -> fc2 by the two static linear kernels."""
     from types import SimpleNamespace as NS
     from qconvnet import ops, quant as Q
