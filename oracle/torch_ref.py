@@ -359,3 +359,23 @@ def build_resnet_static_int8_cpu(fp32, calib_batches, per_channel=True):
             net(xb)
     tq.convert(net, inplace=True)
     return net.eval()
+
+
+def build_optimized_dynamic_cpu(fp32):
+    """/root/reference/models/optimized_custom_quantization.py:26-76 on a
+    torchvision-layout ResNet (shared ``relu`` per Bottleneck, e.g.
+    models.resnet.ResNet): fuse stem conv1+bn1+relu and, per bottleneck,
+    conv2+bn2+relu, conv3+bn3, downsample conv+BN (conv1 left unfused), then
+    quantize_dynamic with default_dynamic_qconfig everywhere (:108-127)."""
+    torch.backends.quantized.engine = "fbgemm"
+    m = copy.deepcopy(fp32).cpu().eval()
+    fuse = [["conv1", "bn1", "relu"]]
+    for name, mod in m.named_modules():
+        if hasattr(mod, "conv3") and hasattr(mod, "bn3"):   # a Bottleneck
+            fuse.append([f"{name}.conv2", f"{name}.bn2", f"{name}.relu"])
+            fuse.append([f"{name}.conv3", f"{name}.bn3"])
+            if mod.downsample is not None:
+                fuse.append([f"{name}.downsample.0", f"{name}.downsample.1"])
+    fused = tq.fuse_modules(m, fuse, inplace=False)
+    return torch.ao.quantization.quantize_dynamic(fused, {"": tq.default_dynamic_qconfig},
+                                                  dtype=torch.qint8)

@@ -198,3 +198,31 @@ def test_inference_benchmark_and_evaluator(sd):
     ev = ModelEvaluator(data.SyntheticLoader(1024, 256, seed=3, labels=labels))
     top1, top5 = ev.evaluate_accuracy(q, verbose=False)
     assert top1 > 80 and top5 >= top1
+
+
+def test_optimized_custom_quantization_dropin():
+    """models.optimized_custom_quantization (reference :7-137): the fused fp32
+    body (its shared-ReLU fusion quirk included) + dynamic int8 fc.  The fc is
+    bit-exact with quantize_dynamic's on the CPU model's own features; end to
+    end the MIOpen-vs-oneDNN fp32 body stays within the stated 1 % bound."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from models.optimized_custom_quantization import OptimizedCustomQuantization
+    from models.resnet import synthetic_images, synthetic_resnet
+    from oracle import torch_ref
+    m = synthetic_resnet(2, (1, 1, 1, 1), num_classes=10, hw=64, calib_images=8)
+    oc = OptimizedCustomQuantization()
+    q = oc.quantize(m)
+    assert q.quantized and q.is_custom_quantized
+    ref = torch_ref.build_optimized_dynamic_cpu(m)
+    x = torch.from_numpy(synthetic_images(32, 7, 64))
+    feats = {}
+    h = ref.fc.register_forward_pre_hook(lambda mod, a: feats.__setitem__("x", a[0].clone()))
+    with torch.no_grad():
+        want = ref(x).numpy()
+    h.remove()
+    got_fc = q.classify(feats["x"].cuda().contiguous()).cpu().numpy()
+    assert np.array_equal(got_fc, want)
+    got = q(x).numpy()
+    assert np.abs(got - want).max() <= REF_MODE_REL_TOL * np.abs(want).max()
+    assert oc.get_model_size(q) > 0
