@@ -273,8 +273,13 @@ class QuantizedConvNet:
             d.z_x, d.z_y, d.s_y, d.relu = int(e["z_x"]), int(e["z_y"]), F32(e["s_y"]), e["relu"]
             setattr(self, name, d)
 
-    def _buffers(self, n):
-        b = self._bufs.get(n)
+    def buffers(self, n, slot=0):
+        """The device activation buffers run() used for batch size n (slot:
+        run_pipelined's buffer set): a2, a4, a6 / a6k, f1, q, logits, ..."""
+        return self._bufs[(n, slot)]
+
+    def _buffers(self, n, slot=0):
+        b = self._bufs.get((n, slot))
         if b is None:
             dev = self.device
             b = {"a1": torch.empty((n, 32, 32, 64), dtype=torch.uint8, device=dev),
@@ -287,7 +292,7 @@ class QuantizedConvNet:
                  "f1f": torch.empty((n, 512), dtype=torch.float32, device=dev),
                  "q": torch.empty((n, 10), dtype=torch.uint8, device=dev),
                  "logits": torch.empty((n, 10), dtype=torch.float32, device=dev)}
-            self._bufs[n] = b
+            self._bufs[(n, slot)] = b
         return b
 
     # --------------------------------------------------------------- forward
@@ -323,7 +328,7 @@ class QuantizedConvNet:
     def _fused(self, x_shape):
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
 
-    def run(self, x, keep=False, marks=None):
+    def run(self, x, keep=False, marks=None, slot=0):
         """Launch the whole int8 forward on the current stream of the model's
         device (no sync).
         Returns the fp32 logits tensor (a reused buffer); with keep=True also
@@ -333,11 +338,11 @@ class QuantizedConvNet:
         if x.device != self.device:
             raise ValueError(f"input on {x.device}, model on {self.device}")
         with torch.cuda.device(self.device):   # ops launch on this device's current stream
-            return self._run(x, keep, marks)
+            return self._run(x, keep, marks, slot)
 
-    def _run(self, x, keep, marks):
+    def _run(self, x, keep, marks, slot=0):
         n = x.shape[0]
-        b = self._buffers(n)
+        b = self._buffers(n, slot)
         L = self.L
 
         def mark():
@@ -422,6 +427,24 @@ class QuantizedConvNet:
             b["ws"] = ops.classifier_workspace(n, f1.w.shape[0], self.device)
         f1.relu, f2.relu = True, False
         return ops.classifier(xk, f1, f2, b["ws"], b["f1"], b["q"], b["logits"])
+
+    def run_pipelined(self, batches, streams):
+        """Forward a sequence of batches with len(streams) of them in flight:
+        batch k runs on streams[k % S] with its own activation buffers (slot
+        k % S), so one batch's launches fill the ramp / drain of another's
+        (every batch still goes through every layer at its own batch size).
+        Returns the logits tensors (reused buffers, one per slot); no sync."""
+        S = len(streams)
+        cur = torch.cuda.current_stream(self.device)
+        for s in streams:
+            s.wait_stream(cur)
+        outs = []
+        for k, x in enumerate(batches):
+            with torch.cuda.stream(streams[k % S]):
+                outs.append(self.run(x, slot=k % S))
+        for s in streams:
+            cur.wait_stream(s)
+        return outs
 
     def capture_graph(self, x_static):
         """Capture run(x_static) into a HIP graph; replay with replay(n)."""

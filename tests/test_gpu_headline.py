@@ -48,7 +48,7 @@ def _headline_model(per_channel, dev):
 def _check_headline_bufs(model, n, z, rows=slice(None)):
     import netfix
     from qconvnet import ops
-    b = model._bufs[n]
+    b = model.buffers(n)
     assert netfix.sha(b["a2"][rows].cpu().numpy()) == str(z["a2_sha"])
     assert netfix.sha(b["a4"][rows].cpu().numpy()) == str(z["a4_sha"])
     a6 = ops.from_kmajor(b["a6k"])[rows].reshape(-1, 4, 4, 256)
@@ -115,7 +115,7 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     tol = 1e-5 * np.abs(z["logits"]).max()
     # default launches: a2, a4, a6, fc1 are the HBM hand-offs
     logits = model.run(xd).cpu().numpy()
-    b = model._bufs[n]
+    b = model.buffers(n)
     for a in ("a2", "a4", "a6"):
         assert netfix.sha(b[a].cpu().numpy()) == str(z[f"{a}_sha"]), a
     assert netfix.sha(b["f1"].cpu().numpy()) == str(z["fc1_sha"])
@@ -142,3 +142,22 @@ def test_model_on_second_device(golden_dir):
     out = model.run(x)
     torch.cuda.synchronize("cuda:1")
     assert np.array_equal(out.cpu().numpy(), z["logits"])
+
+
+def test_run_pipelined_equals_sequential(dev, golden_dir):
+    """Two batches in flight on two streams (run_pipelined, one activation
+    buffer set per stream): every batch's logits equal its own single-stream
+    run, and the first equals the torch.ao fixture."""
+    from oracle import torch_ref
+    z = _fixture(golden_dir, "net_static_int8_b1024.npz")
+    model = _headline_model(False, dev)
+    xs = [torch.from_numpy(torch_ref.synthetic_images(1024, s)).to(dev) for s in (0, 11, 12, 13)]
+    want = [model.run(x).clone() for x in xs]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    got = []
+    for k in range(0, 4, 2):   # the slot buffers are reused every len(streams) batches
+        got += [o.clone() for o in model.run_pipelined(xs[k:k + 2], streams)]
+    torch.cuda.synchronize()
+    for g, w in zip(got, want):
+        assert torch.equal(g, w)
+    assert np.array_equal(got[0].cpu().numpy(), z["logits"])

@@ -439,11 +439,11 @@ def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
     model = QuantizedConvNet(spec, dev)
     assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
-    a4_p = model._bufs[x.shape[0]]["a4"].clone()
+    a4_p = model.buffers(x.shape[0])["a4"].clone()
     model.fuse_pairs = False
     out_l = model.run(x).clone()
     torch.cuda.synchronize()
-    assert torch.equal(a4_p, model._bufs[x.shape[0]]["a4"])
+    assert torch.equal(a4_p, model.buffers(x.shape[0])["a4"])
     assert torch.equal(out_p, out_l)
 
 
@@ -463,12 +463,12 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     model = QuantizedConvNet(spec, dev)
     assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
-    b = model._bufs[n]
+    b = model.buffers(n)
     a4_p = b["a4"].clone()
     a6_p = (ops.from_kmajor(b["a6k"]).clone() if model._head_fused(n) else b["a6"].reshape(n, -1).clone())
     model.fuse_pairs = False
     out_l = model.run(x).clone()
-    b = model._bufs[n]
+    b = model.buffers(n)
     a6_l = (ops.from_kmajor(b["a6k"]) if model._head_fused(n) else b["a6"].reshape(n, -1))
     torch.cuda.synchronize()
     assert torch.equal(a4_p, b["a4"])
