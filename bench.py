@@ -43,6 +43,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec at batch 1024 (3×32×32) int8 static-PTQ, 1/2/4/8 MI355X; top-1 delta"
+METRIC_QDQ = "images/sec at batch 256 (3×32×32) per-layer QDQ int8 conv (CustomQuantizationModel), 1 MI355X"
 PEAK_INT8_TOPS = 5033.0   # 256 CU x 4 SIMD x 2048 int8 op/clk x 2.4 GHz (dense)
 PEAK_HBM_GBS = 8000.0
 # MAC per image per kernel
@@ -72,10 +73,11 @@ HBM_BOUND = {"conv1"}
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
                   "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256",),
-                  "fc12": ("fc_splitk_kernel", "fc_finish_kernel")}
+                  "fc12": ("fc_splitk_kernel", "fc_finish_kernel"),
+                  "fc1": ("linear_u8s8_kernel",), "fc2": ("linear_f32_kernel",)}
 
 
-def build_model(rank, device, per_channel=False, spec_file=None):
+def build_model(rank, device, per_channel=False, spec_file=None, mode="static"):
     from models.baseline_model import trained_synthetic_model
     from qconvnet import data
     from qconvnet.dist import broadcast_object
@@ -91,13 +93,15 @@ def build_model(rank, device, per_channel=False, spec_file=None):
         fp = trained_synthetic_model(0, device=device)
         folded = fold_state_dict(fp.state_dict())
         ranges = calibrate(folded, [calib], "cpu")
-        payload = (build_qspec(folded, ranges, "static", per_channel), fp.state_dict())
+        payload = (build_qspec(folded, ranges, mode, per_channel), fp.state_dict())
     spec, sd = broadcast_object(payload)
     return QuantizedConvNet(spec, device), sd
 
 
 def cpu_baselines(state_dict, qmodel_gpu, seconds):
     """Reference CPU paths on the host cores (rank 0, N = 1 only)."""
+    if qmodel_gpu.mode == "qdq":
+        return cpu_baseline_qdq(state_dict, qmodel_gpu, seconds)
     from oracle import torch_ref
     from qconvnet import data
     fp = torch_ref.SimpleConvNetRef()
@@ -176,6 +180,52 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
     return out
 
 
+def cpu_baseline_qdq(state_dict, qmodel_gpu, seconds):
+    """configs[1]'s CPU counterpart: the per-layer QDQ net (every conv and fc1
+    QuantStub -> int8 op -> DeQuantStub, fp32 ReLU / pool / fc2,
+    custom_quantization_model.py:202-261) with its stubs converted by torch.ao
+    (fbgemm), batch 256, on the host cores; and the top-1 of both on the
+    held-out synthetic set."""
+    from oracle import torch_ref
+    from qconvnet import data
+    fp = torch_ref.SimpleConvNetRef()
+    fp.load_state_dict(state_dict)
+    fp.eval()
+    threads = torch.get_num_threads()
+    calib = torch.from_numpy(data.synthetic_task(512, 1)[0])
+    q = torch_ref.build_qdq_cpu(fp, [calib])
+    bs = 256
+    x = torch.from_numpy(data.synthetic_images(bs, 12))
+    with torch.no_grad():
+        q(x)
+        total, iters = 0.0, 0
+        while total < seconds:
+            t0 = time.time()
+            q(x)
+            total += time.time() - t0
+            iters += 1
+    out = {"static_ptq": {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
+                          "kind": "port",
+                          "sample": f"BASELINE configs[1] on the CPU: per-layer QDQ SimpleConvNet "
+                                    f"(torch.ao fbgemm, stubs converted), batch {bs} x {iters} iters"}}
+    xe_np, ye_np = data.synthetic_task(4096, 77)
+    xe, lab = torch.from_numpy(xe_np), torch.from_numpy(ye_np)
+    with torch.no_grad():
+        fp_pred = fp(xe).argmax(1)
+        gpu_pred = qmodel_gpu(xe).argmax(1)
+        cpu_pred = q(xe).argmax(1)
+
+    def acc(p):
+        return (p == lab).float().mean().item() * 100
+
+    out["top1"] = {"labels": "true labels of 4096 held-out images of the synthetic 10-class task",
+                   "fp32": acc(fp_pred), "gpu_int8_qdq": acc(gpu_pred),
+                   "cpu_torchao_qdq": acc(cpu_pred),
+                   "delta_vs_cpu_qdq_pct": acc(gpu_pred) - acc(cpu_pred),
+                   "argmax_agreement_gpu_vs_cpu_qdq_pct": (gpu_pred == cpu_pred).float().mean().item() * 100}
+    return out
+
+
 # ------------------------------------------------------------ PMC passes
 # HBM traffic, MFMA busy and the clock the chip holds come from rocprofv3
 # counter passes over a child run of this script (same model, same batch),
@@ -189,7 +239,7 @@ PMC_PASSES = (("fetch", ("FETCH_SIZE",), None),
               ("clock", ("GRBM_GUI_ACTIVE",), 8192))
 
 
-def _pmc_child(counters, batch, spec_file, per_channel, timeout):
+def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static"):
     """One rocprofv3 --pmc pass over `bench.py --no-cpu --no-pmc` as a child
     process (never an exec).  Returns ({kernel: {counter: mean per dispatch}},
     the child's JSON line) or raises."""
@@ -202,6 +252,8 @@ def _pmc_child(counters, batch, spec_file, per_channel, timeout):
            "1", "--no-cpu", "--no-pmc", "--batch", str(batch), "--spec-file", spec_file]
     if per_channel:
         cmd.append("--per-channel")
+    if mode != "static":
+        cmd += ["--workload", "qdq"]
     env = dict(os.environ, TMPDIR="/tmp")
     p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                          text=True, start_new_session=True)
@@ -252,7 +304,7 @@ def pmc_counters(model, sd, args, names, timeout=150):
         for tag, counters, batch in PMC_PASSES:
             try:
                 agg, child = _pmc_child(counters, batch or args.batch, spec_file, args.per_channel,
-                                        timeout)
+                                        timeout, model.mode)
             except Exception as e:   # a failed pass leaves its fields null
                 errors.append(f"{tag}: {e}")
                 continue
@@ -290,7 +342,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1024, help="images per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="images per GPU (default 1024; 256 for --workload qdq, 512 for resnet50)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true",
@@ -300,9 +353,12 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the forward as one HIP graph (measured: no gain, the launch "
                          "queue already runs back to back)")
-    ap.add_argument("--workload", choices=("convnet", "resnet50"), default="convnet",
-                    help="convnet: BASELINE configs[2]/[3] (the metric); resnet50: configs[4]")
+    ap.add_argument("--workload", choices=("convnet", "qdq", "resnet50"), default="convnet",
+                    help="convnet: BASELINE configs[2]/[3] (the metric); qdq: configs[1] (per-layer "
+                         "QDQ CustomQuantizationModel, batch 256); resnet50: configs[4]")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = {"convnet": 1024, "qdq": 256, "resnet50": 512}[args.workload]
     if args.workload == "resnet50":
         return main_resnet(args)
 
@@ -315,7 +371,8 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
 
-    model, sd = build_model(rank, dev, args.per_channel, args.spec_file)
+    mode = "qdq" if args.workload == "qdq" else "static"
+    model, sd = build_model(rank, dev, args.per_channel, args.spec_file, mode)
     B = args.batch
     x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
     gathered = torch.empty((world * B, 10), dtype=torch.float32, device=dev) if world > 1 else None
@@ -408,12 +465,15 @@ def main():
         roof["pmc_error"] = pmc_err
 
     result = {
-        "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": world,
+        "metric": METRIC if mode == "static" else METRIC_QDQ, "value": value, "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int8", "data": "synthetic",
-        "config": {"workload": "full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
-                               "NHWC, per-tensor weights" + (" [per-channel]" if args.per_channel else ""),
+        "config": {"workload": ("full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
+                                "NHWC, per-tensor weights" if mode == "static" else
+                                "per-layer QDQ SimpleConvNet (CustomQuantizationModel, BASELINE configs[1]): "
+                                "every conv and fc1 int8 with the dequantize/ReLU/pool/quantize hand-off "
+                                "fused, fp32 fc2") + (" [per-channel]" if args.per_channel else ""),
                    "global_batch": world * B, "per_gpu_batch": B, "image": [3, 32, 32],
                    "parallelism": f"dp{world}", "collective": "all_gather logits (RCCL)" if world > 1 else None},
         "roofline": roof,
@@ -423,7 +483,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baselines(sd, model, args.cpu_seconds)
         result["cpu_baseline"] = cb["static_ptq"]
-        result["cpu_static_int8"] = cb["static_int8"]
+        if "static_int8" in cb:
+            result["cpu_static_int8"] = cb["static_int8"]
         result["top1"] = cb["top1"]
         result["gpu_vs_cpu_ratio"] = value / cb["static_ptq"]["value"]
     if rank == 0:
@@ -480,7 +541,7 @@ def main_resnet(args):
     rank, world, local = qd.init()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B = args.batch if args.batch != 1024 else 512
+    B = args.batch
     fp = synthetic_resnet(0, device=dev, calib_images=32)
     calib = [torch.from_numpy(synthetic_images(32, 1 + i)) for i in range(2)]
     model = quantize_resnet(fp, calib, dev, per_channel=True)

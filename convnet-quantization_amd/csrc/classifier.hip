@@ -200,6 +200,107 @@ __global__ __launch_bounds__(256) void fc_finish_kernel(const int* __restrict__ 
   }
 }
 
+// Wave sum of v over the 64 lanes by DPP (quad xor 1 / 2, half-row and row
+// mirrors, row broadcasts 15 / 31); the total lands in lane 63.
+QCN_DEV float wave_sum_dpp(float v) {
+#define QCN_DPP_ADD(CTL, RM) \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTL, RM, 0xF, false))
+  QCN_DPP_ADD(0xB1, 0xF);
+  QCN_DPP_ADD(0x4E, 0xF);
+  QCN_DPP_ADD(0x141, 0xF);
+  QCN_DPP_ADD(0x140, 0xF);
+  QCN_DPP_ADD(0x142, 0xA);
+  QCN_DPP_ADD(0x143, 0xC);
+#undef QCN_DPP_ADD
+  return v;
+}
+
+// QDQ variant of the finisher (CustomQuantizedSimpleConvNet,
+// custom_quantization_model.py:256-258): fc1's stub chain requantizes to its
+// own output qparams (no ReLU in the int8 op), DeQuantStub ->
+// fp32(s1) * (q1 - z1), F.relu in fp32, then fc2 stays an fp32 nn.Linear:
+// y = x @ w2^T + b2.  Each lane holds 8 of the 512 fc1 features; fc2's dot
+// products are lane-local fma chains summed over the wave (fp32, a different
+// summation order from MKL's sgemm: the QDQ tests bound it).
+struct FcHeadQdq {
+  const float *u1, *v1, *m1;
+  const int* corr1;
+  int z1, lo1;
+  float s1;
+  const float* w2;   // [n2][512] fp32
+  const float* b2;   // [n2] or nullptr
+  int n2;
+};
+
+__global__ __launch_bounds__(256) void fc_finish_qdq_kernel(const int* __restrict__ part, int m,
+                                                            FcHeadQdq hd, uint8_t* __restrict__ y1,
+                                                            float* __restrict__ y2f) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= m) return;
+  const int f0 = lane * 8;
+  int4 pv[FC_S][2];
+#pragma unroll
+  for (int s = 0; s < FC_S; ++s) {
+    const int* p = part + ((long)s * m + row) * FC_N1 + f0;
+    pv[s][0] = *reinterpret_cast<const int4*>(p);
+    pv[s][1] = *reinterpret_cast<const int4*>(p + 4);
+  }
+  const int4 c0 = *reinterpret_cast<const int4*>(hd.corr1 + f0), c1 = *reinterpret_cast<const int4*>(hd.corr1 + f0 + 4);
+  const float4 u0 = *reinterpret_cast<const float4*>(hd.u1 + f0), u4 = *reinterpret_cast<const float4*>(hd.u1 + f0 + 4);
+  const float4 v0 = *reinterpret_cast<const float4*>(hd.v1 + f0), v4 = *reinterpret_cast<const float4*>(hd.v1 + f0 + 4);
+  const float4 m0 = *reinterpret_cast<const float4*>(hd.m1 + f0), m4 = *reinterpret_cast<const float4*>(hd.m1 + f0 + 4);
+  int a[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+  for (int s = 0; s < FC_S; ++s) {
+    a[0] += pv[s][0].x; a[1] += pv[s][0].y; a[2] += pv[s][0].z; a[3] += pv[s][0].w;
+    a[4] += pv[s][1].x; a[5] += pv[s][1].y; a[6] += pv[s][1].z; a[7] += pv[s][1].w;
+  }
+  const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u4.x, u4.y, u4.z, u4.w};
+  const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v4.x, v4.y, v4.z, v4.w};
+  const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m4.x, m4.y, m4.z, m4.w};
+  int q[8];
+  float xf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    q[e] = requant_one(a[e], uu[e], vv[e], mm[e], hd.z1, hd.lo1);
+    const float d = (float)(q[e] - hd.z1) * hd.s1;   // aten::dequantize
+    xf[e] = d > 0.f ? d : 0.f;                       // F.relu
+  }
+  if (y1) {
+    const uint32_t lo = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    const uint32_t hw = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
+    *reinterpret_cast<uint2*>(y1 + (long)row * FC_N1 + f0) = make_uint2(lo, hw);
+  }
+  float acc[FC_N2];
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) {
+    acc[o] = 0.f;
+    if (o < hd.n2) {
+      const float4 wa = *reinterpret_cast<const float4*>(hd.w2 + (long)o * FC_N1 + f0);
+      const float4 wb = *reinterpret_cast<const float4*>(hd.w2 + (long)o * FC_N1 + f0 + 4);
+      float t = xf[0] * wa.x;
+      t = __builtin_fmaf(xf[1], wa.y, t);
+      t = __builtin_fmaf(xf[2], wa.z, t);
+      t = __builtin_fmaf(xf[3], wa.w, t);
+      t = __builtin_fmaf(xf[4], wb.x, t);
+      t = __builtin_fmaf(xf[5], wb.y, t);
+      t = __builtin_fmaf(xf[6], wb.z, t);
+      t = __builtin_fmaf(xf[7], wb.w, t);
+      acc[o] = t;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) acc[o] = wave_sum_dpp(acc[o]);
+  float mine = 0.f;
+#pragma unroll
+  for (int o = 0; o < FC_N2; ++o) {
+    const float tot = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc[o]), 63));
+    if (lane == o) mine = tot;
+  }
+  if (lane < hd.n2) y2f[(long)row * hd.n2 + lane] = mine + (hd.b2 ? hd.b2[lane] : 0.f);
+}
+
 }  // namespace qcn
 
 extern "C" {
@@ -237,6 +338,26 @@ int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1
                  y2_zp, relu2 ? y2_zp : 0, y2_scale};
   hipLaunchKernelGGL(qcn::fc_finish_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd, y1,
                      y2, y2f);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_classifier_qdq_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1,
+                            const float* u1, const float* v1, const float* mult1,
+                            const int32_t* corr1, int y1_zp, float y1_scale, const float* w2,
+                            int n2, const float* b2, void* workspace, uint8_t* y1, float* y2,
+                            void* stream) {
+  if (!x || !w1 || !u1 || !v1 || !mult1 || !corr1 || !w2 || !workspace || !y2) return QCN_ERR_ARG;
+  if (m <= 0 || k <= 0 || n1 <= 0 || n2 <= 0 || y1_zp < 0 || y1_zp > 255 || !(y1_scale > 0.f))
+    return QCN_ERR_ARG;
+  if (m % 128 != 0 || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 || n2 > qcn::FC_N2)
+    return QCN_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  int* part = static_cast<int*>(workspace);
+  const int tiles = (m / 128) * (n1 / 64) * qcn::FC_S;
+  hipLaunchKernelGGL(qcn::fc_splitk_kernel, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
+  qcn::FcHeadQdq hd{u1, v1, mult1, corr1, y1_zp, 0, y1_scale, w2, b2, n2};
+  hipLaunchKernelGGL(qcn::fc_finish_qdq_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd,
+                     y1, y2);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

@@ -233,21 +233,37 @@ __global__ void quantize_legacy_kernel(const float* __restrict__ x, long long co
   }
 }
 
-__global__ void linear_f32_kernel(const float* __restrict__ x, int m, int k,
-                                  const float* __restrict__ w, int n, const float* __restrict__ b,
-                                  int relu_in, float* __restrict__ y) {
-  const long total = (long)m * n;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
-       e += (long)gridDim.x * blockDim.x) {
-    const int f = (int)(e % n);
-    const long row = e / n;
-    float acc = 0.f;
-    for (int kk = 0; kk < k; ++kk) {
-      float xv = x[row * k + kk];
+// One wave per row: lane l takes k-elements l, l + 64, ...; up to 16 outputs
+// per pass (fma chains per lane, then a wave reduction by xor shuffles).
+__global__ __launch_bounds__(256) void linear_f32_kernel(const float* __restrict__ x, int m, int k,
+                                                         const float* __restrict__ w, int n,
+                                                         const float* __restrict__ b, int relu_in,
+                                                         float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= m) return;
+  const float* xr = x + row * k;
+  for (int f0 = 0; f0 < n; f0 += 16) {
+    float acc[16];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) acc[o] = 0.f;
+    for (int kk = lane; kk < k; kk += 64) {
+      float xv = xr[kk];
       if (relu_in) xv = xv > 0.f ? xv : 0.f;
-      acc = __builtin_fmaf(xv, w[(long)f * k + kk], acc);
+#pragma unroll
+      for (int o = 0; o < 16; ++o)
+        if (f0 + o < n) acc[o] = __builtin_fmaf(xv, w[(long)(f0 + o) * k + kk], acc[o]);
     }
-    y[e] = acc + (b ? b[f] : 0.f);
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+    }
+    float mine = 0.f;
+#pragma unroll
+    for (int o = 0; o < 16; ++o)
+      if (lane == o) mine = acc[o];
+    if (lane < 16 && f0 + lane < n) y[row * n + f0 + lane] = mine + (b ? b[f0 + lane] : 0.f);
   }
 }
 
@@ -339,10 +355,8 @@ int qcn_linear_dynamic_range_f32(const float* x, int m, int k, const int8_t* w, 
 int qcn_linear_f32(const float* x, int m, int k, const float* w, int n, const float* b,
                    int relu_in, float* y, void* stream) {
   if (!x || !w || !y || m <= 0 || k <= 0 || n <= 0) return QCN_ERR_ARG;
-  const long total = (long)m * n;
-  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(qcn::linear_f32_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, m,
-                     k, w, n, b, relu_in, y);
+  hipLaunchKernelGGL(qcn::linear_f32_kernel, dim3((m + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     x, m, k, w, n, b, relu_in, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 

@@ -64,6 +64,8 @@ SIGNATURES = {
                                       i32, vp, vp]),
     "qcn_classifier_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp,
                                   vp, i32, i32, f32, vp, vp, vp, vp, vp]),
+    "qcn_classifier_qdq_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp,
+                                      vp, vp, vp, vp]),
     "qcn_pack_conv_weight_kmajor": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_conv_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
                                  vp, vp, vp, vp, i32, i32, vp, vp]),

@@ -273,6 +273,23 @@ def classifier(xk, l1, l2, workspace, y1, y2, y2f):
     return True
 
 
+def classifier_qdq(xk, l1, l2, workspace, y1, y2f):
+    """QDQ head (BASELINE config 2): fc1 int8 -> requant -> dequantize ->
+    ReLU -> fp32 fc2, two launches.  ``l1`` as for classifier() (wk, u, v,
+    mult, corr, z_y, s_y); ``l2`` carries the fp32 w [n2, n1] and b.  Returns
+    False outside the kernel's envelope (caller falls back)."""
+    _need(xk, torch.uint8, "classifier_qdq.x")
+    kc, m, _ = xk.shape
+    rc = lib().qcn_classifier_qdq_u8s8(_ptr(xk), m, kc * 32, _ptr(l1.wk), l1.wk.shape[1], _ptr(l1.u),
+                                       _ptr(l1.v), _ptr(l1.mult), _ptr(l1.corr), int(l1.z_y),
+                                       float(l1.s_y), _ptr(l2.w), l2.w.shape[0], _ptr(l2.b),
+                                       _ptr(workspace), _ptr(y1), _ptr(y2f), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "classifier_qdq")
+    return True
+
+
 def minmax_range(x, out=None):
     """[min, max] of a device fp32 tensor as a device float[2] (A2 kernel)."""
     _need(x, torch.float32, "minmax.x")

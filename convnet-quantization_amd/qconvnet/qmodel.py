@@ -306,7 +306,7 @@ class QuantizedConvNet:
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
             names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
-        if self._head_fused(x_shape[0]):
+        if self._head(x_shape[0], keep):
             names = names[:-2] + ["fc12"]
         return tuple(names)
 
@@ -321,9 +321,17 @@ class QuantizedConvNet:
         if os.environ.get("QCN_FC_HEAD", "fused") == "linear":   # A/B switch (tools/ab.sh)
             return False
         c6 = self.L[5]
-        return (self.mode == "static" and n % 128 == 0 and f1.w.shape[0] == 512 and
-                f1.w.shape[1] == 4096 and hasattr(f1, "wk") and f2.w.shape[0] <= 16 and
-                f2.z_x == f1.z_y and c6.qdq is None and c6.cout == 256 and c6.pool)
+        common = (n % 128 == 0 and f1.w.shape[0] == 512 and f1.w.shape[1] == 4096 and
+                  hasattr(f1, "wk") and f2.w.shape[0] <= 16 and c6.cout == 256 and c6.pool)
+        if self.mode == "qdq":   # conv6's QDQ hand-off writes fc1's u8 input chunk-major
+            return common
+        return common and self.mode == "static" and f2.z_x == f1.z_y and c6.qdq is None
+
+    def _head(self, n, keep):
+        """The split-K classifier head runs (in QDQ mode only behind the conv5+6
+        pair, whose epilogue applies conv6's QDQ hand-off to the chunk-major
+        output; the per-layer chunk-major conv6 has no hand-off)."""
+        return self._head_fused(n) and (self.mode != "qdq" or self._pairs(keep))
 
     def _fused(self, x_shape):
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
@@ -354,7 +362,7 @@ class QuantizedConvNet:
         mark()
         d = L[0]
         names = ["a2", "a3", "a4", "a5", "a6"]
-        head = self._head_fused(n)
+        head = self._head(n, keep)
         if self._fused(x.shape):
             ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
             mark()
@@ -420,11 +428,14 @@ class QuantizedConvNet:
 
     def _classifier(self, xk, b):
         """fc1+ReLU -> fc2 -> dequantize in two launches (split-K fc1 on the
-        chunk-major conv6 output + a per-row finisher)."""
+        chunk-major conv6 output + a per-row finisher); in QDQ mode fc1's
+        dequantize, ReLU and the fp32 fc2 run in the finisher."""
         f1, f2 = self.fc1, self.fc2
         n = xk.shape[1]
         if "ws" not in b:
             b["ws"] = ops.classifier_workspace(n, f1.w.shape[0], self.device)
+        if self.mode == "qdq":
+            return ops.classifier_qdq(xk, f1, f2, b["ws"], b["f1"], b["logits"])
         f1.relu, f2.relu = True, False
         return ops.classifier(xk, f1, f2, b["ws"], b["f1"], b["q"], b["logits"])
 

@@ -175,6 +175,20 @@ int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1
                         const float* mult2, int y2_zp, int relu2, float y2_scale, void* workspace,
                         uint8_t* y1, uint8_t* y2, float* y2_deq, void* stream);
 
+/* QDQ classifier head (CustomQuantizedSimpleConvNet, BASELINE config 2;
+ * custom_quantization_model.py:218-219, 256-258): fc1's QuantStub -> int8
+ * Linear -> requant to (y1_scale, y1_zp) (no ReLU in the int8 op) ->
+ * DeQuantStub -> F.relu (fp32) -> fc2 as an fp32 nn.Linear (w2 fp32 [n2][n1],
+ * b2 fp32 [n2] or NULL) -> y2 fp32 [m][n2].  y1 (optional) receives fc1's u8
+ * output.  Same split-K first launch, layouts, envelope and workspace as
+ * qcn_classifier_u8s8; fc2's fp32 sums run in a different order from a CPU
+ * sgemm (the QDQ tests bound the difference). */
+int qcn_classifier_qdq_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1,
+                            const float* u1, const float* v1, const float* mult1,
+                            const int32_t* corr1, int y1_zp, float y1_scale, const float* w2,
+                            int n2, const float* b2, void* workspace, uint8_t* y1, float* y2,
+                            void* stream);
+
 /* A8 — quantized::linear_dynamic (DynamicQuantizedLinear of
  * models/static_ptq_model.py:28-32 and models/dynamic_ptq_model.py:302-306):
  * per-call activation qparams from the batch min/max (ChooseQuantizationParams,

@@ -102,6 +102,7 @@ def test_batch_8192_shards_equal_1024(dev, golden_dir):
 def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     import netfix
     from oracle import torch_ref
+    from qconvnet import ops
     from qconvnet.qmodel import QuantizedConvNet
     z = _fixture(golden_dir, "net_qdq_b256.npz")
     spec = netfix.qdq_spec(netfix.load(False))
@@ -113,11 +114,15 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     names = model.kernel_names(xd.shape)
     assert names[:3] == ("conv12", "conv34", "conv56"), names
     tol = 1e-5 * np.abs(z["logits"]).max()
-    # default launches: a2, a4, a6, fc1 are the HBM hand-offs
+    # default launches: a2, a4, a6 (chunk-major for the split-K head), fc1
+    # are the HBM hand-offs
+    assert names[3:] == ("fc12",), names
     logits = model.run(xd).cpu().numpy()
     b = model.buffers(n)
-    for a in ("a2", "a4", "a6"):
+    for a in ("a2", "a4"):
         assert netfix.sha(b[a].cpu().numpy()) == str(z[f"{a}_sha"]), a
+    a6 = ops.from_kmajor(b["a6k"]).view(n, 4, 4, 256)
+    assert netfix.sha(a6.cpu().numpy()) == str(z["a6_sha"])
     assert netfix.sha(b["f1"].cpu().numpy()) == str(z["fc1_sha"])
     assert np.abs(logits - z["logits"]).max() <= tol
     assert np.array_equal(logits.argmax(1), z["argmax"])
@@ -126,7 +131,35 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     logits2, b = m2.run(xd, keep=True)
     for i in range(1, 7):
         assert netfix.sha(b[f"a{i}"].cpu().numpy()) == str(z[f"a{i}_sha"]), i
-    assert np.array_equal(logits2.cpu().numpy(), logits)
+    assert netfix.sha(b["f1"].cpu().numpy()) == str(z["fc1_sha"])
+    # per-layer fc2 (linear_f32) sums in another fp32 order than the head
+    assert np.abs(logits2.cpu().numpy() - z["logits"]).max() <= tol
+    assert np.array_equal(logits2.cpu().numpy().argmax(1), z["argmax"])
+
+
+def test_qdq_head_equals_two_linears(dev, golden_dir, monkeypatch):
+    """QDQ split-K head (fc1 int8 -> dequantize -> ReLU -> fp32 fc2 in the
+    finisher) against the per-layer fc1 (linear_u8s8) + fp32 fc2
+    (linear_f32) launches on the same conv6 output: fc1's u8 output
+    identical, fp32 logits within the stated fp32 tolerance (different
+    summation orders), same argmax; at 384 images (3 row blocks)."""
+    import netfix
+    from oracle import torch_ref
+    from qconvnet.qmodel import QuantizedConvNet
+    spec = netfix.qdq_spec(netfix.load(False))
+    x = torch.from_numpy(torch_ref.synthetic_images(384, 5)).to(dev)
+    model = QuantizedConvNet(spec, dev)
+    assert model.kernel_names(x.shape)[-1] == "fc12"
+    head = model.run(x).clone()
+    f1_head = model.buffers(384)["f1"].clone()
+    monkeypatch.setenv("QCN_FC_HEAD", "linear")
+    assert model.kernel_names(x.shape)[-2:] == ("fc1", "fc2")
+    lin = model.run(x).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(f1_head, model.buffers(384)["f1"])
+    tol = 1e-5 * lin.abs().max().item()
+    assert (head - lin).abs().max().item() <= tol
+    assert torch.equal(head.argmax(1), lin.argmax(1))
 
 
 def test_model_on_second_device(golden_dir):
