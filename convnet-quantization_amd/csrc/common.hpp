@@ -27,6 +27,17 @@ inline int qcn_current_device() {
   int d = 0;
   return (hipGetDevice(&d) == hipSuccess && d >= 0 && d < QCN_MAX_DEV) ? d : -1;
 }
+// Compute units of the current device (cached per device); 0 on error.
+inline int qcn_cu_count() {
+  static int ncu_dev[QCN_MAX_DEV] = {};
+  const int d = qcn_current_device();
+  if (d < 0) return 0;
+  int& ncu = ncu_dev[d];
+  if (!ncu && (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess ||
+               ncu <= 0))
+    ncu = 0;
+  return ncu;
+}
 inline bool qcn_set_lds_once(const void* kernel, int lds_bytes, bool (&done)[QCN_MAX_DEV]) {
   const int d = qcn_current_device();
   if (d < 0) return false;

@@ -1495,6 +1495,15 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
+    // four images per 8-wave workgroup (one per CU: the conv6 patch and ring
+    // fill the LDS); below four images per CU that leaves CUs idle, so small
+    // batches take two images per 4-wave workgroup (same wave tile and
+    // patch layout, twice the workgroups)
+    const int ncu = qcn_cu_count();
+    if (ncu > 0 && nimg < 4 * ncu)
+      return launch_pair<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
+                         ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
                        ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);

@@ -90,17 +90,28 @@ class CustomQuantizedResNet50:
     s8 weights, MinMax-calibrated u8 activations).  ``calibration_batches``:
     an iterable of fp32 [N,3,H,W] tensors (or (x, y) pairs); default 32
     synthetic ImageNet-normalised 224x224 images.  ``conv1_scale`` is accepted
-    for signature compatibility; the reference never uses it."""
+    for signature compatibility; the reference never uses it.
+
+    mode="static" (default): the static int8 executor above.  mode="reference":
+    the reference's own block semantics (:60-143) with its per-layer stubs
+    live — every conv QuantStub -> int8 conv -> DeQuantStub, BN / ReLU /
+    max-pool / residual add / avg-pool in fp32 between them, nothing folded —
+    as ``qconvnet.resnet_qdq.QuantizedResNetQDQ``."""
 
     def __init__(self, model, conv1_scale=1.0, calibration_batches=None, device="cuda",
-                 per_channel=True):
+                 per_channel=True, mode="static"):
         from qconvnet.resnet import quantize_resnet
+        from qconvnet.resnet_qdq import quantize_resnet_reference
         from models.resnet import synthetic_images
+        if mode not in ("static", "reference"):
+            raise ValueError(f"unknown mode {mode!r}")
         if calibration_batches is None:
             calibration_batches = [torch.from_numpy(synthetic_images(32, 1))]
         batches = [b[0] if isinstance(b, (tuple, list)) else b for b in calibration_batches]
         self.conv1_scale = conv1_scale
-        self.quantized_model = quantize_resnet(model.eval(), batches, device, per_channel)
+        self.mode = mode
+        build = quantize_resnet if mode == "static" else quantize_resnet_reference
+        self.quantized_model = build(model.eval(), batches, device, per_channel)
 
     def __call__(self, x):
         return self.quantized_model(x)

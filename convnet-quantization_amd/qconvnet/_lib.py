@@ -64,6 +64,12 @@ SIGNATURES = {
                                       i32, vp, vp]),
     "qcn_classifier_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp,
                                   vp, i32, i32, f32, vp, vp, vp, vp, vp]),
+    "qcn_dq_bn_q_u8": (i32, [vp, i64, i32, f32, i32, vp, vp, i32, f32, i32, vp, vp]),
+    "qcn_dq_bn_relu_maxpool_f32": (i32, [vp, i32, i32, i32, i32, f32, i32, vp, vp, vp, f32, i32, vp,
+                                         vp]),
+    "qcn_qdq_join_f32": (i32, [vp, f32, i32, vp, vp, vp, f32, i32, vp, vp, vp, i64, i32, vp, f32, i32,
+                               vp, vp]),
+    "qcn_avgpool_f32_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_classifier_qdq_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp,
                                       vp, vp, vp, vp]),
     "qcn_pack_conv_weight_kmajor": (i32, [vp, i32, i32, i32, i32, vp, vp]),

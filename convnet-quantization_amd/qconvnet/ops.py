@@ -443,3 +443,61 @@ def avgpool(x, x_zp, out=None):
         out = torch.empty((n, c), dtype=torch.uint8, device=x.device)
     check(lib().qcn_avgpool_u8_nhwc(_ptr(x), n, h * w, c, int(x_zp), _ptr(out), _stream()), "avgpool")
     return out
+
+
+# -------------------------- §8(f)2 in the reference's semantics (live stubs)
+def dq_bn_q(y, s, z, alpha, beta, relu, s_next, z_next, out=None):
+    """conv u8 -> DeQuantStub -> BN -> [ReLU] -> the next conv's QuantStub."""
+    _need(y, torch.uint8, "dq_bn_q.y")
+    if out is None:
+        out = torch.empty_like(y)
+    check(lib().qcn_dq_bn_q_u8(_ptr(y), y.numel(), y.shape[-1], float(s), int(z), _ptr(alpha),
+                               _ptr(beta), int(bool(relu)), float(s_next), int(z_next), _ptr(out),
+                               _stream()), "dq_bn_q")
+    return out
+
+
+def dq_bn_relu_maxpool(y, s, z, alpha, beta, s_next=None, z_next=0):
+    """Stem hand-off: fp32 max-pool 3x3/2 of relu(bn(dq(y))) and (s_next given)
+    its u8 quantize.  Returns (fp32 map, u8 map or None)."""
+    _need(y, torch.uint8, "dq_bn_relu_maxpool.y")
+    n, h, w, c = y.shape
+    shape = (n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c)
+    out = torch.empty(shape, dtype=torch.float32, device=y.device)
+    oq = torch.empty(shape, dtype=torch.uint8, device=y.device) if s_next is not None else None
+    check(lib().qcn_dq_bn_relu_maxpool_f32(_ptr(y), n, h, w, c, float(s), int(z), _ptr(alpha),
+                                           _ptr(beta), _ptr(out), float(s_next or 0.0), int(z_next),
+                                           _ptr(oq), _stream()), "dq_bn_relu_maxpool")
+    return out, oq
+
+
+def qdq_join(y3, s3, z3, a3, b3, ident, s_next=None, z_next=0):
+    """Residual join: relu(bn3(dq(y3)) + identity); ``ident`` is either the
+    fp32 block input or (yd, sd, zd, ad, bd) of the downsample conv.
+    Returns (fp32 block output, u8 quantize for the next stubs or None)."""
+    _need(y3, torch.uint8, "qdq_join.y3")
+    out = torch.empty(y3.shape, dtype=torch.float32, device=y3.device)
+    oq = torch.empty_like(y3) if s_next is not None else None
+    if isinstance(ident, tuple):
+        yd, sd, zd, ad, bd = ident
+        _need(yd, torch.uint8, "qdq_join.yd")
+        idf = None
+    else:
+        _need(ident, torch.float32, "qdq_join.identity")
+        yd, sd, zd, ad, bd, idf = None, 0.0, 0, None, None, ident
+    ref = yd if yd is not None else idf
+    if tuple(ref.shape) != tuple(y3.shape):
+        raise ValueError("identity shape differs from conv3's output")
+    check(lib().qcn_qdq_join_f32(_ptr(y3), float(s3), int(z3), _ptr(a3), _ptr(b3), _ptr(yd), float(sd),
+                                 int(zd), _ptr(ad), _ptr(bd), _ptr(idf), y3.numel(), y3.shape[-1],
+                                 _ptr(out), float(s_next or 0.0), int(z_next), _ptr(oq), _stream()),
+          "qdq_join")
+    return out, oq
+
+
+def avgpool_f32(x):
+    _need(x, torch.float32, "avgpool_f32.x")
+    n, h, w, c = x.shape
+    out = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    check(lib().qcn_avgpool_f32_nhwc(_ptr(x), n, h, w, c, _ptr(out), _stream()), "avgpool_f32")
+    return out

@@ -75,10 +75,28 @@ def bn_eval_affine(mean, var, gamma, beta, eps=1e-5):
     gamma, beta = np.asarray(gamma, f32), np.asarray(beta, f32)
     invstd = (f32(1.0) / np.sqrt(var + f32(eps))).astype(f32)
     alpha = (invstd * gamma).astype(f32)
-    # the float64 product of two fp32 values is exact; one rounding to fp32
-    # after the add reproduces fma except in double-rounding corner cases
-    bprime = (beta.astype(np.float64) - mean.astype(np.float64) * alpha.astype(np.float64)).astype(f32)
-    return alpha, bprime
+    return alpha, fmaf_host(-mean, alpha, beta)
+
+
+def fmaf_host(a, b, c):
+    """fl32(a*b + c) with one rounding, vectorised on the host: a*b is exact
+    in float64, the sum rounds once to float64, and when that double lands
+    exactly on an fp32 midpoint the TwoSum error term decides the direction
+    (the one case where double rounding would differ)."""
+    a64 = np.asarray(a, F32).astype(np.float64)
+    b64 = np.asarray(b, F32).astype(np.float64)
+    c64 = np.asarray(c, F32).astype(np.float64)
+    p = a64 * b64
+    s = p + c64
+    bb = s - p
+    e = (p - (s - bb)) + (c64 - bb)
+    r = s.astype(F32)
+    r64 = r.astype(np.float64)
+    diff = s - r64
+    nxt = np.nextafter(r, np.where(diff > 0, np.inf, -np.inf).astype(F32))
+    mid = (diff != 0) & (s == (r64 + nxt.astype(np.float64)) * 0.5)
+    fix = mid & (e != 0) & (np.sign(e) == np.sign(diff))
+    return np.where(fix, nxt, r).astype(F32)
 
 
 def quantize_weight(w, scale):

@@ -267,6 +267,37 @@ int qcn_stem_pack_f32_nchw(const float* x, int nimg, int h, int w, float scale, 
 int qcn_avgpool_u8_nhwc(const uint8_t* x, int nimg, int hw, int c, int x_zp, uint8_t* y,
                         void* stream);
 
+/* ---- SURVEY §8(f)2 in the reference's own semantics ----------------------
+ * CustomQuantizedBottleneck / CustomQuantizedResNet50 with live per-layer
+ * stubs (models/custom_quantization_model.py:34-45, 60-143): fp32 BN / ReLU /
+ * max-pool / residual add / avg-pool between int8 convs
+ * (qcn_conv_gemm_u8s8_nhwc, requant to each conv's own output qparams, no
+ * ReLU).  All maps NHWC, C % 4 == 0; alpha / beta are BN's eval constants
+ * (ATen: alpha = fp32(fp32(1/sqrt(var+eps)) * gamma), beta = fmaf(-mean,
+ * alpha, bias); the map is fmaf(x, alpha, beta)); every quantize is
+ * zp + rint(x * fp32(1/s)) clamped to [0, 255]; ReLU keeps -0.0 (torch.relu).
+ * Pointers: u8 4-B aligned, fp32 maps and alpha / beta 16-B aligned. */
+/* conv -> DeQuantStub -> BN -> [ReLU] -> next conv's QuantStub (u8 -> u8). */
+int qcn_dq_bn_q_u8(const uint8_t* y, long long count, int c, float s, int z, const float* alpha,
+                   const float* beta, int relu, float s_next, int z_next, uint8_t* out,
+                   void* stream);
+/* Stem: conv -> DeQuantStub -> BN -> ReLU -> MaxPool2d(3, 2, 1): fp32
+ * [n][(h-1)/2+1][(w-1)/2+1][c] (the first block's input and identity), plus,
+ * when out_q is not NULL, that map quantized for block 0's QuantStubs. */
+int qcn_dq_bn_relu_maxpool_f32(const uint8_t* y, int n, int h, int w, int c, float s, int z,
+                               const float* alpha, const float* beta, float* out, float s_next,
+                               int z_next, uint8_t* out_q, void* stream);
+/* Residual join (:92-101): out = relu(bn3(dq(y3)) + identity), identity =
+ * bn_d(dq(yd)) (downsample conv, yd != NULL) or the fp32 block input idf;
+ * fp32 out, plus out_q (optional) quantized for the next block's stubs. */
+int qcn_qdq_join_f32(const uint8_t* y3, float s3, int z3, const float* a3, const float* b3,
+                     const uint8_t* yd, float sd, int zd, const float* ad, const float* bd,
+                     const float* idf, long long count, int c, float* out, float s_next, int z_next,
+                     uint8_t* out_q, void* stream);
+/* AdaptiveAvgPool2d(1) on fp32 NHWC: sequential fp32 sum over the window in
+ * row-major order, then / (h*w) (ATen's channels-last kernel) -> [n][c]. */
+int qcn_avgpool_f32_nhwc(const float* x, int n, int h, int w, int c, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

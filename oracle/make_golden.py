@@ -548,6 +548,112 @@ def gen_resnet_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
     return rec
 
 
+def _resnet_qdq_spec_from_torchao(q):
+    """The oracle's reference-semantics ResNet spec (qref.resnet_qdq_forward's
+    format = qconvnet.resnet_qdq.build_spec's) read out of a converted
+    RefQDQResNet: per stub (s_x, z_x), per int8 conv its weights, scales,
+    output qparams and geometry, per BN its eval constants."""
+    def conv(m, bn):
+        op = m.op
+        wq = op.weight()
+        b = op.bias()
+        e = dict(w=wq.int_repr().numpy(), s_w=wq.q_per_channel_scales().numpy().astype(F32),
+                 b=(np.zeros(wq.shape[0], F32) if b is None else b.detach().numpy().astype(F32)),
+                 s_x=F32(m.quant.scale.item()), z_x=int(m.quant.zero_point.item()),
+                 s_y=F32(op.scale), z_y=int(op.zero_point))
+        if bn is not None:
+            e["stride"], e["pad"] = tuple(op.stride), tuple(op.padding)
+            e["bn"] = qref.bn_eval_constants(bn.running_mean.numpy(), bn.running_var.numpy(),
+                                             bn.weight.detach().numpy(), bn.bias.detach().numpy(), bn.eps)
+        return e
+
+    spec = {"per_channel": True, "stem": conv(q.conv1, q.bn1), "blocks": []}
+    for li in range(1, 5):
+        for blk in getattr(q, f"layer{li}"):
+            e = {k: conv(getattr(blk, k), getattr(blk, "bn" + k[-1])) for k in ("conv1", "conv2", "conv3")}
+            e = {"c1": e["conv1"], "c2": e["conv2"], "c3": e["conv3"], "ds": None}
+            if blk.downsample is not None:
+                e["ds"] = conv(blk.downsample[0], blk.downsample[1])
+            spec["blocks"].append(e)
+    spec["fc"] = conv(q.fc, None)
+    return spec
+
+
+def gen_resnet_qdq_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
+    """§8(f)2 in the reference's own semantics: the same 1-1-1-1 ResNet at
+    64x64 as CustomQuantizedResNet50 with live per-layer stubs
+    (torch_ref.RefQDQResNet, torch.ao eager, fbgemm, CPU calibration):
+    fp32 BN / ReLU / max-pool / residual add / avg-pool between int8 convs.
+    Stores every stub's and conv's qparams, int8-weight hashes, every conv's
+    u8 output and every block's fp32 output by hash, the fc's u8 output and
+    the logits; asserts the numpy oracle (qref.resnet_qdq_forward)
+    reproduces every one bit for bit."""
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    imnet = dict(mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), hw=hw)
+    fp = tr.ResNetRef(layers, num_classes)
+    fp.load_state_dict(tr.resnet_state_dict(fp, 0))
+    tr.recalibrate_bn(fp, torch.from_numpy(tr.synthetic_images(16, 3, **imnet)))
+    calib = tr.synthetic_images(8, 4, **imnet)
+    q = tr.build_resnet_qdq_cpu(fp, [torch.from_numpy(calib)])
+    x = tr.synthetic_images(n, 5, **imnet)
+    outs, hooks = {}, []
+
+    def grab(mod, key):
+        hooks.append(mod.register_forward_hook(lambda m, a, o: outs.__setitem__(key, o)))
+
+    grab(q.conv1.op, "stem.q")
+    grab(q.maxpool, "stem")
+    grab(q.avgpool, "pool")
+    grab(q.fc.op, "fc.q")
+    bi = 0
+    for li in range(1, 5):
+        for blk in getattr(q, f"layer{li}"):
+            for k in ("conv1", "conv2", "conv3"):
+                grab(getattr(blk, k).op, f"block{bi}.c{k[-1]}")
+            if blk.downsample is not None:
+                grab(blk.downsample[0].op, f"block{bi}.ds")
+            grab(blk, f"block{bi}")
+            bi += 1
+    with torch.no_grad():
+        logits = q(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    spec = _resnet_qdq_spec_from_torchao(q)
+    mine, inter = qref.resnet_qdq_forward(x, spec, keep=True)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().numpy()  # noqa: E731
+    rec = {"layers": np.asarray(layers, np.int64), "hw": np.int64(hw), "batch": np.int64(n),
+           "num_classes": np.int64(num_classes), "x_sha": sha(x), "calib_sha": sha(calib),
+           "logits": logits}
+    for k, t in outs.items():
+        if k == "pool":
+            ref = t.reshape(n, -1).numpy()
+        elif t.is_quantized:
+            ref = t.int_repr().numpy() if t.dim() == 2 else nhwc(t.int_repr())
+        else:
+            ref = nhwc(t)
+        assert ref.dtype == inter[k].dtype and (ref == inter[k]).all(), k
+        rec[k + "_sha"] = sha(inter[k])
+    assert (mine == logits).all(), "logits"
+    rec["q_logits"] = inter["fc.q"]
+    for k, v in fp.state_dict().items():   # BN running statistics (the recalibrated state)
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            rec["sd." + k] = v.numpy()
+
+    def put(name, e):
+        rec[name + ".s_x"], rec[name + ".z_x"] = F32(e["s_x"]), np.int64(e["z_x"])
+        rec[name + ".s_y"], rec[name + ".z_y"] = F32(e["s_y"]), np.int64(e["z_y"])
+        rec[name + ".w_sha"] = sha(e["w"])
+    put("stem", spec["stem"])
+    for i, e in enumerate(spec["blocks"]):
+        for k in ("c1", "c2", "c3", "ds"):
+            if e[k] is not None:
+                put(f"b{i}.{k}", e[k])
+    put("fc", spec["fc"])
+    np.savez_compressed(os.path.join(OUT, "net_resnet_qdq.npz"), **rec)
+    return rec
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.backends.quantized.engine = "fbgemm"
@@ -556,6 +662,9 @@ def main():
         return
     if sys.argv[1:] == ["resnet_net"]:   # only the §8(f)2 whole-net vectors
         gen_resnet_net()
+        return
+    if sys.argv[1:] == ["resnet_qdq"]:   # only the §8(f)2 reference-semantics vectors
+        gen_resnet_qdq_net()
         return
     if sys.argv[1:] == ["headline"]:   # only the batch-1024 / batch-256 whole-net vectors
         gen_net_headline(per_channel=False)
@@ -575,6 +684,7 @@ def main():
     gen_qdq_config2()
     gen_resnet_ops(np.random.Generator(np.random.PCG64(4321)))
     gen_resnet_net()
+    gen_resnet_qdq_net()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 

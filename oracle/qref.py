@@ -479,3 +479,92 @@ def resnet_int8_forward(x_nchw, spec, keep=False):
     u, v, mult = requant_constants(fc["s_x"], fc["s_w"], fc["s_y"], fc["b"])
     qy = linear_q(q, fc["z_x"], fc["w"], u, v, mult, fc["z_y"], False)
     return dequantize(qy, fc["s_y"], fc["z_y"]), inter
+
+
+# ----------------------------------------------- §8(f)2, reference semantics
+def bn_eval_constants(mean, var, gamma, beta, eps=1e-5):
+    """ATen CPU batch_norm (eval) as the torch 2.10 wheel computes it
+    (batch_norm_kernel.cpp batch_norm_cpu_collect_linear_and_constant_terms,
+    probed bit-exact here on contiguous and channels-last maps):
+    invstd = fp32(1 / sqrt(fp32(var + eps))), alpha = fp32(invstd * gamma),
+    beta' = fmaf(-mean, alpha, beta); the map is y = fmaf(x, alpha, beta')."""
+    var = np.asarray(var, F32)
+    invstd = (F32(1.0) / np.sqrt((var + F32(eps)).astype(F32))).astype(F32)
+    alpha = (invstd * np.asarray(gamma, F32)).astype(F32)
+    return alpha, fmaf(-np.asarray(mean, F32), alpha, np.asarray(beta, F32))
+
+
+def bn_eval_nhwc(x, alpha, beta):
+    return fmaf(x, alpha[None, None, None, :], beta[None, None, None, :])
+
+
+def relu_f32(x):
+    """torch.relu / F.relu on fp32: x where not x < 0, so -0.0 stays -0.0
+    (np.maximum(-0.0, 0.0) would return +0.0)."""
+    return np.where(x < 0, F32(0.0), x).astype(F32)
+
+
+def maxpool3x3s2_f32_nhwc(x):
+    """nn.MaxPool2d(3, 2, padding=1) on fp32 (padding = -inf)."""
+    n, h, w, c = x.shape
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    xp = np.full((n, h + 2, w + 2, c), -np.inf, F32)
+    xp[:, 1:h + 1, 1:w + 1, :] = x
+    out = np.full((n, oh, ow, c), -np.inf, F32)
+    for r in range(3):
+        for s in range(3):
+            out = np.maximum(out, xp[:, r:r + 2 * (oh - 1) + 1:2, s:s + 2 * (ow - 1) + 1:2, :])
+    return out
+
+
+def avgpool_f32_nhwc(x):
+    """AdaptiveAvgPool2d(1) on an fp32 channels-last map (ATen
+    cpu_adaptive_avg_pool channels-last kernel): sequential fp32 sum over the
+    window in row-major order, then fp32(sum / (H*W))."""
+    n, h, w, c = x.shape
+    acc = np.zeros((n, c), F32)
+    for i in range(h):
+        for j in range(w):
+            acc = (acc + x[:, i, j, :]).astype(F32)
+    return (acc / F32(h * w)).astype(F32)
+
+
+def _qdq_conv(x_f32, e):
+    """QuantStub -> int8 conv (requant to the conv's output qparams, no ReLU)
+    -> DeQuantStub -> BN (fp32)."""
+    q = quantize_per_tensor(x_f32, e["s_x"], e["z_x"])
+    u, v, mult = requant_constants(e["s_x"], e["s_w"], e["s_y"], e["b"])
+    y = conv_q(q, e["z_x"], e["w"], u, v, mult, e["z_y"], False, tuple(e["stride"]), tuple(e["pad"]))
+    return y, bn_eval_nhwc(dequantize(y, e["s_y"], e["z_y"]), *e["bn"])
+
+
+def resnet_qdq_forward(x_nchw, spec, keep=False):
+    """CustomQuantizedResNet50 with live per-layer stubs
+    (custom_quantization_model.py:60-143): fp32 NHWC activations between the
+    layers, each conv quantized at its own stub.  ``spec`` layout:
+    qconvnet.resnet_qdq.build_spec.  Returns (logits fp32, inter) — inter
+    holds every conv's u8 output and every block's fp32 output."""
+    inter = {}
+    x = nchw_to_nhwc(np.asarray(x_nchw, F32))
+    y, f = _qdq_conv(x, spec["stem"])
+    inter["stem.q"] = y
+    x = maxpool3x3s2_f32_nhwc(relu_f32(f))
+    inter["stem"] = x
+    for i, blk in enumerate(spec["blocks"]):
+        y1, f = _qdq_conv(x, blk["c1"])
+        y2, f = _qdq_conv(relu_f32(f), blk["c2"])
+        y3, out = _qdq_conv(relu_f32(f), blk["c3"])
+        idn = x
+        if blk.get("ds") is not None:
+            yd, idn = _qdq_conv(x, blk["ds"])
+            inter[f"block{i}.ds"] = yd
+        x = relu_f32((out + idn).astype(F32))
+        inter.update({f"block{i}.c1": y1, f"block{i}.c2": y2, f"block{i}.c3": y3, f"block{i}": x})
+    p = avgpool_f32_nhwc(x)
+    inter["pool"] = p
+    fc = spec["fc"]
+    q = quantize_per_tensor(p, fc["s_x"], fc["z_x"])
+    u, v, mult = requant_constants(fc["s_x"], fc["s_w"], fc["s_y"], fc["b"])
+    qy = linear_q(q, fc["z_x"], fc["w"], u, v, mult, fc["z_y"], False)
+    inter["fc.q"] = qy
+    return dequantize(qy, fc["s_y"], fc["z_y"]), inter

@@ -361,6 +361,66 @@ def build_resnet_static_int8_cpu(fp32, calib_batches, per_channel=True):
     return net.eval()
 
 
+class RefQDQBottleneck(nn.Module):
+    """CustomQuantizedBottleneck (/root/reference/models/custom_quantization_model.py
+    :60-102) with its stubs live: every conv (and the downsample conv) is
+    QuantStub -> int8 conv -> DeQuantStub (:34-45), BN and ReLU stay fp32
+    modules, the residual add is a float add (:95-101)."""
+
+    def __init__(self, b):
+        super().__init__()
+        self.conv1, self.bn1 = _QDQConv(b.conv1), b.bn1
+        self.conv2, self.bn2 = _QDQConv(b.conv2), b.bn2
+        self.conv3, self.bn3 = _QDQConv(b.conv3), b.bn3
+        self.downsample = (None if b.downsample is None else
+                           nn.Sequential(_QDQConv(b.downsample[0]), b.downsample[1]))
+
+    def forward(self, x):
+        identity = x
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return F.relu(out + identity)
+
+
+class RefQDQResNet(nn.Module):
+    """CustomQuantizedResNet50 (:104-143) around a ResNetRef with the per-layer
+    stubs live.  The outer QuantStub / DeQuantStub (:107-108, :127, :142) stay
+    identities: converted, the outer QuantStub would hand conv1's own
+    QuantStub an already-quantized tensor, which torch rejects."""
+
+    def __init__(self, fp):
+        super().__init__()
+        self.conv1, self.bn1, self.maxpool = _QDQConv(fp.conv1), fp.bn1, fp.maxpool
+        for i in range(1, 5):
+            setattr(self, f"layer{i}", nn.Sequential(*[RefQDQBottleneck(b) for b in getattr(fp, f"layer{i}")]))
+        self.avgpool, self.fc = fp.avgpool, _QDQConv(fp.fc)
+
+    def forward(self, x):
+        x = self.maxpool(F.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def build_resnet_qdq_cpu(fp32, calib_batches, per_channel=True):
+    """torch.ao eager conversion of RefQDQResNet (fbgemm): each stub's MinMax
+    observer sees the fp32 network's activations during calibration, as
+    prepare() runs the unquantized forward; per-channel symmetric s8 weights."""
+    torch.backends.quantized.engine = "fbgemm"
+    net = RefQDQResNet(copy.deepcopy(fp32).eval()).eval()
+    for m in net.modules():
+        if isinstance(m, _QDQConv):
+            m.qconfig = static_qconfig(per_channel)
+    tq.prepare(net, inplace=True)
+    with torch.no_grad():
+        for xb in calib_batches:
+            net(xb)
+    tq.convert(net, inplace=True)
+    return net.eval()
+
+
 def build_optimized_dynamic_cpu(fp32):
     """/root/reference/models/optimized_custom_quantization.py:26-76 on a
     torchvision-layout ResNet (shared ``relu`` per Bottleneck, e.g.

@@ -23,8 +23,58 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-def load():
-    return dict(np.load(os.path.join(HERE, "golden", "net_resnet_int8.npz")))
+def load(name="net_resnet_int8.npz"):
+    return dict(np.load(os.path.join(HERE, "golden", name)))
+
+
+def load_qdq():
+    """The reference-semantics (live per-layer stubs) fixture,
+    oracle/make_golden.py gen_resnet_qdq_net."""
+    return load("net_resnet_qdq.npz")
+
+
+def qdq_spec(z, fixture_qparams=False):
+    """Product spec (qconvnet.resnet_qdq.build_spec) from the fixture's
+    regenerated fp32 model, calibrated by the PRODUCT host code on the
+    fixture's calibration images.  fixture_qparams=True then overwrites every
+    stub's and conv's qparams with the fixture's: the calibration's fp32 CPU
+    convs differ in the last bits between host CPUs (the GPU box's is not this
+    container's), so GPU tests take torch.ao's qparams as given, as
+    spec() does for the static net; the CPU test pins the calibration here."""
+    from qconvnet import resnet_qdq
+    net = resnet_qdq.unfolded_state(fp32_model(z).state_dict())
+    ranges = resnet_qdq.calibrate(net, [torch.from_numpy(images(z, "calib"))], "cpu")
+    sp = resnet_qdq.build_spec(net, ranges, True)
+    if fixture_qparams:
+        def put(name, e):
+            e["s_x"], e["z_x"] = F32(z[name + ".s_x"]), int(z[name + ".z_x"])
+            e["s_y"], e["z_y"] = F32(z[name + ".s_y"]), int(z[name + ".z_y"])
+        put("stem", sp["stem"])
+        for i, e in enumerate(sp["blocks"]):
+            for k in ("c1", "c2", "c3", "ds"):
+                if e[k] is not None:
+                    put(f"b{i}.{k}", e[k])
+        put("fc", sp["fc"])
+    return sp
+
+
+def check_qdq_spec(sp, z):
+    """Names whose qparams or int8 weights differ from torch.ao's."""
+    bad = []
+
+    def cmp(name, e):
+        for k in ("s_x", "z_x", "s_y", "z_y"):
+            if np.asarray(e[k]) != np.asarray(z[f"{name}.{k}"]):
+                bad.append(f"{name}.{k}")
+        if sha(e["w"]) != str(z[f"{name}.w_sha"]):
+            bad.append(f"{name}.w")
+    cmp("stem", sp["stem"])
+    for i, e in enumerate(sp["blocks"]):
+        for k in ("c1", "c2", "c3", "ds"):
+            if e[k] is not None:
+                cmp(f"b{i}.{k}", e[k])
+    cmp("fc", sp["fc"])
+    return bad
 
 
 def fp32_model(z):

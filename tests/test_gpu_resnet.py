@@ -223,3 +223,42 @@ def test_custom_quantized_resnet50_wrapper(dev):
     # calibration runs on the CPU by default: a second quantization is identical
     again = quantize_resnet(m, calib, dev)
     assert np.array_equal(again(torch.from_numpy(x)).numpy(), out.numpy())
+
+
+def test_resnet_reference_semantics_equals_torchao_fixture(dev):
+    """§8(f)2 in the reference's own semantics on the GPU
+    (CustomQuantizedResNet50 with live per-layer stubs,
+    custom_quantization_model.py:60-143; tests/golden/net_resnet_qdq.npz):
+    every int8 conv's u8 output, the stem's and every block's fp32 output
+    (BN / ReLU / max-pool / residual add in fp32), the fc's u8 output and the
+    fp32 logits bit-exact to torch.ao eager (fbgemm) — the fp32 hand-offs use
+    ATen's op order, so no tolerance is needed."""
+    import resnetfix
+    from qconvnet.resnet_qdq import QuantizedResNetQDQ
+    z = resnetfix.load_qdq()
+    sp = resnetfix.qdq_spec(z, fixture_qparams=True)
+    assert resnetfix.check_qdq_spec(sp, z) == []
+    qm = QuantizedResNetQDQ(sp, dev)
+    logits, inter = qm.run(torch.from_numpy(resnetfix.images(z)).to(dev), keep=True)
+    torch.cuda.synchronize()
+    keys = [k[:-4] for k in z if k.endswith("_sha") and not k.endswith(".w_sha")
+            and k not in ("x_sha", "calib_sha")]
+    assert "block3" in keys and "stem.q" in keys and "fc.q" in keys
+    for k in keys:
+        assert resnetfix.sha(inter[k].cpu().numpy()) == str(z[k + "_sha"]), k
+    assert np.array_equal(logits.cpu().numpy(), z["logits"])
+
+
+def test_custom_quantized_resnet50_reference_mode(dev):
+    """CustomQuantizedResNet50(mode="reference") builds the live-stub executor
+    and equals the numpy oracle (qref.resnet_qdq_forward) on its own spec."""
+    from models.custom_quantization_model import CustomQuantizedResNet50
+    from models.resnet import synthetic_images, synthetic_resnet
+    m = synthetic_resnet(2, (1, 1, 1, 1), num_classes=10, hw=64, calib_images=8, device=dev)
+    calib = [torch.from_numpy(synthetic_images(8, 7, 64))]
+    w = CustomQuantizedResNet50(m, calibration_batches=calib, device=dev, mode="reference")
+    x = synthetic_images(5, 8, 64)
+    out = w(torch.from_numpy(x))
+    assert out.shape == (5, 10) and out.device.type == "cpu"
+    ref, _ = qref.resnet_qdq_forward(x, w.quantized_model.spec)
+    assert np.array_equal(out.numpy(), ref)

@@ -98,3 +98,32 @@ def test_product_cpu_calibration_reproduces_torchao_qparams():
         assert (np.float32(e["out"][0]), e["out"][1]) == (np.float32(z[f"b{i}.out_scale"]),
                                                           int(z[f"b{i}.out_zp"])), i
     assert (sp["fc"]["s_y"], sp["fc"]["z_y"]) == (np.float32(z["fc.s_y"]), int(z["fc.z_y"]))
+
+
+def test_reference_semantics_oracle_and_host_spec_pinned():
+    """§8(f)2 in the reference's semantics (CustomQuantizedResNet50 with live
+    per-layer stubs, fp32 BN / ReLU / add / pools between int8 convs): the
+    PRODUCT host code (unfolded weights, CPU calibration, qparams, per-channel
+    int8 weights, BN eval constants) reproduces torch.ao's converted model,
+    and the numpy oracle run on that spec reproduces every conv's u8 output,
+    every block's fp32 output and the logits of the golden bit for bit."""
+    import hashlib
+    import resnetfix
+    z = resnetfix.load_qdq()
+    sp = resnetfix.qdq_spec(z)
+    assert resnetfix.check_qdq_spec(sp, z) == []
+    logits, inter = qref.resnet_qdq_forward(resnetfix.images(z), sp, keep=True)
+    for k in [k[:-4] for k in z if k.endswith("_sha") and not k.endswith(".w_sha")
+              and k not in ("x_sha", "calib_sha")]:
+        assert hashlib.sha256(np.ascontiguousarray(inter[k]).tobytes()).hexdigest() == str(z[k + "_sha"]), k
+    assert np.array_equal(logits, z["logits"])
+
+
+def test_bn_eval_constants_product_equals_oracle():
+    from qconvnet import quant as Q
+    rng = np.random.default_rng(3)
+    m, v, g, b = (rng.standard_normal(256).astype(np.float32) for _ in range(4))
+    v = np.abs(v) + np.float32(0.01)
+    pa, pb = Q.bn_eval_affine(m, v, g, b)
+    oa, ob = qref.bn_eval_constants(m, v, g, b)
+    assert np.array_equal(pa, oa) and np.array_equal(pb, ob)
