@@ -233,6 +233,18 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     const v2f s3 = {a.s3, a.s3};
     const int rr = tid / TPR, cq = tid % TPR;   // phase-2 row / 16-column group
     const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i
+    // the identity bytes of both halves' phase 2, loaded before phase 1 so
+    // their HBM latency hides behind the requant math (rows past npix: 0)
+    constexpr int NIT = C::BM / RPI;
+    uint4 rid[2][NIT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const long p = m0 + it * RPI + rr;
+        rid[i][it] = p < a.npix ? *reinterpret_cast<const uint4*>(a.r + p * a.cout + ch2 + 32 * i)
+                                : make_uint4(0u, 0u, 0u, 0u);
+      }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int co0 = n0 + wc * 64 + i * 32;
@@ -268,13 +280,13 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
       const float zof = (float)a.z_o;
       auto join = [&](auto zo0) {
         constexpr bool ZO0 = decltype(zo0)::value;   // z_o == 0: ReLU = saturation at 0
-#pragma unroll 2
-        for (int r0 = 0; r0 < C::BM; r0 += RPI) {
-          const int row = r0 + rr;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int row = it * RPI + rr;
           const long p = m0 + row;
           if (p >= a.npix) break;
           const long off = p * a.cout + ch2 + 32 * i;
-          const uint4 rv = *reinterpret_cast<const uint4*>(a.r + off);
+          const uint4 rv = rid[i][it];
           const float4* dp = reinterpret_cast<const float4*>(lds + row * OSF + cq * 64);
           const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
           uint32_t ow[4];
