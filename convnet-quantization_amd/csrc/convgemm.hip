@@ -186,34 +186,59 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   const int swz = (l32 >> 2) & 3;
   const int boff0 = C::AREG + (wm * C::JT) * 2048 + l32 * 64 + ((hi ^ swz) << 4);
   const int boff1 = C::AREG + (wm * C::JT) * 2048 + l32 * 64 + (((2 + hi) ^ swz) << 4);
-  for (int st = 0; st < nst; ++st) {
-    __builtin_amdgcn_sched_barrier(0);
-    if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (st + 2 < nst) issue(st + 2);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint8_t* buf = lds + (st % 3) * C::STAGE;
+  auto rd_a = [&](int st, int c, int i) {
+    return *reinterpret_cast<const v4i*>(lds + (st % 3) * C::STAGE + (c * (BN / 32) + wc * 2 + i) * 1024 +
+                                         lane * 16);
+  };
+  auto rd_b = [&](int st, int c, int j) {
+    return *reinterpret_cast<const v4i*>(lds + (st % 3) * C::STAGE + (c ? boff1 : boff0) + j * 2048);
+  };
+  // Software pipeline over half-stages (one 32-byte K chunk each): the
+  // fragments of the next half-stage are read one per MFMA of this one.  The
+  // ring's one barrier per stage sits between its two halves: it certifies
+  // stage st+1 landed (its reads start in the second half) and that every
+  // wave is done with stage st-1, whose buffer stage st+2's DMA then reuses.
+  auto seg = [&](const v4i (&fa)[2], v4i (&fb)[C::JT], v4i (&na)[2], v4i (&nb)[C::JT], int rst,
+                 int rc, bool rd) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      v4i fa[2], fb[C::JT];
+    for (int j = 0; j < C::JT; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const v4i*>(buf + (c * (BN / 32) + wc * 2 + i) * 1024 + lane * 16);
+      for (int d = 0; d < 4; ++d) fb[j][d] ^= (int)0x80808080u;   // u8 -> s8 (q - 128)
 #pragma unroll
-      for (int j = 0; j < C::JT; ++j) {
-        v4i b = *reinterpret_cast<const v4i*>(buf + (c ? boff1 : boff0) + j * 2048);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) b[d] ^= (int)0x80808080u;
-        fb[j] = b;
+    for (int m = 0; m < 2 * C::JT; ++m) {
+      if (rd) {
+        if (m < 2) na[m] = rd_a(rst, rc, m);
+        else if (m < 2 + C::JT) nb[m - 2] = rd_b(rst, rc, m - 2);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < C::JT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[m / C::JT][m % C::JT] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / C::JT], fb[m % C::JT], acc[m / C::JT][m % C::JT], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  v4i fa0[2], fb0[C::JT], fa1[2], fb1[C::JT];
+  if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) fa0[i] = rd_a(0, 0, i);
+#pragma unroll
+  for (int j = 0; j < C::JT; ++j) fb0[j] = rd_b(0, 0, j);
+  for (int st = 0; st < nst; ++st) {
+    // first half: multiply (st, 0), read (st, 1)
+    seg(fa0, fb0, fa1, fb1, st, 1, true);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = st + 1 < nst;
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage st+1 (the only DMA in flight)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < nst) issue(st + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // second half: multiply (st, 1), read (st+1, 0)
+    seg(fa1, fb1, fa0, fb0, st + 1, 0, more);
   }
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();   // every wave is done with the ring: reuse it
