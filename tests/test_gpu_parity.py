@@ -475,3 +475,27 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     assert torch.equal(a6_p, a6_l)
     assert torch.equal(out_p, out_l)
     assert np.array_equal(out_p.cpu().numpy(), z["logits"])
+
+
+@pytest.mark.parametrize("n", [1, 6, 300, 1023, 1028])
+def test_conv56_pair_workgroup_shapes_equal_layerwise(dev, n):
+    """conv5+conv6 pair at batch sizes around its two tilings: fewer than four
+    images per CU takes two images per 4-wave workgroup (1, 6, 300, 1023,
+    the last workgroup holding one image when n is odd); from 1024 on four
+    images per 8-wave workgroup (1028: a ragged last workgroup).  conv6's
+    output and the logits equal the per-layer kernels' bit for bit."""
+    import netfix
+    from qconvnet.qmodel import QuantizedConvNet
+    from oracle import torch_ref
+    spec, _ = netfix.static_spec(netfix.load(False))
+    x = torch.from_numpy(torch_ref.synthetic_images(n, 13)).to(dev)
+    model = QuantizedConvNet(spec, dev)
+    assert model.kernel_names(x.shape)[2] == "conv56"
+    out_p = model.run(x).clone()
+    a6_p = model.buffers(n)["a6"].clone()
+    model.fuse_pairs = False
+    out_l = model.run(x).clone()
+    a6_l = model.buffers(n)["a6"]
+    torch.cuda.synchronize()
+    assert torch.equal(a6_p, a6_l)
+    assert torch.equal(out_p, out_l)
