@@ -418,17 +418,34 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   for (int i = 0; i < WI; ++i) fa0[i] = rd_a(0, 0, i);
 #pragma unroll
   for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
+  // Stagger (8-wave workgroups): the second half of the waves (4-7, the
+  // SIMD partners of 0-3, working on the other pixel half) passes each ring
+  // barrier one K-step EARLIER in its program — before step (ch, 0) instead
+  // of (ch, 1) — and issues chunk ch+2's DMA in step (ch, 0), so it runs one
+  // K-step behind its partner and the two no longer reach their reads,
+  // barrier waits and epilogues together (MI355X_MICROARCH 'two waves per
+  // SIMD', item 9).  Hazards as before: barrier c still certifies chunk c
+  // landed (every wave waited for its own pieces) and every wave done with
+  // chunk c-2's buffer (the lagging half consumed its last fragments of it
+  // in the step before the barrier); both halves pass NCH + 1 barriers.
+  // Same-box conv5+6 51.4 -> 47.9 us (profiles/r02_diag_stagger_step_ab.txt);
+  // a whole-chunk stagger measured slower (r02_diag_stagger_chunk_ab.txt).
+  const bool lag = C::NWAVES >= 8 && wave_u >= C::NWAVES / 2;
+  auto ring_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
 #pragma unroll
   for (int ch = 0; ch < C::NCH; ++ch) {
+    if (lag && ch + 1 < C::NCH) ring_barrier();
     // step (ch, 0): read (ch, 1), multiply (ch, 0)
-    step(fa1, fb1, ch, 1, true, fa0, fb0, false, 0);
+    step(fa1, fb1, ch, 1, true, fa0, fb0, lag && ch + 2 < C::NCH, ch + 2);
     if (ch + 1 < C::NCH) {
       // step (ch, 1): chunk ch+1 landed and visible -> read (ch+1, 0), multiply (ch, 1)
-      __builtin_amdgcn_sched_barrier(0);   // chunk ch-1's reads stay before the barrier
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      step(fa0, fb0, ch + 1, 0, true, fa1, fb1, ch + 2 < C::NCH, ch + 2);
+      if (!lag) ring_barrier();   // chunk ch-1's reads stay before the barrier
+      step(fa0, fb0, ch + 1, 0, true, fa1, fb1, !lag && ch + 2 < C::NCH, ch + 2);
     } else {
       step(fa0, fb0, 0, 0, false, fa1, fb1, false, 0);
     }
