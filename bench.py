@@ -93,7 +93,10 @@ def build_model(rank, device, per_channel=False, spec_file=None, mode="static"):
         fp = trained_synthetic_model(0, device=device)
         folded = fold_state_dict(fp.state_dict())
         ranges = calibrate(folded, [calib], "cpu")
-        payload = (build_qspec(folded, ranges, mode, per_channel), fp.state_dict())
+        # host copies: the payload is pickled to every rank, and GPU tensors
+        # would unpickle onto rank 0's device in every process
+        payload = (build_qspec(folded, ranges, mode, per_channel),
+                   {k: v.detach().cpu() for k, v in fp.state_dict().items()})
     spec, sd = broadcast_object(payload)
     return QuantizedConvNet(spec, device), sd
 

@@ -26,8 +26,9 @@ def init(backend=None):
     WORLD_SIZE 1).  Returns (rank, world, local_rank)."""
     rank, world, local = env_rank()
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:   # QCN_DIST_BACKEND=gloo: rehearsal of N ranks on one GPU
+            backend = os.environ.get("QCN_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local)

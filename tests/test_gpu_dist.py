@@ -91,3 +91,44 @@ def test_two_rank_static_product_equals_one_process(dev):
     want = model(torch.from_numpy(torch_ref.synthetic_images(2048, 3))).numpy()
     assert np.array_equal(got, want)
 
+
+
+def _bench_worker(rank, port, q):
+    """bench.py's own N = 2 path (rank-0 model build + spec broadcast, per-rank
+    resident batch, HIP forward, logits all-gather inside the timed step,
+    barrier + max-over-ranks timing), both ranks on cuda:0 over gloo."""
+    _setup(rank, port)
+    os.environ["QCN_DIST_BACKEND"] = "gloo"
+    try:
+        import contextlib
+        import io
+        import json
+        import sys
+        import bench
+        sys.argv = ["bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "256",
+                    "--no-cpu", "--no-pmc"]
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            bench.main()
+        line = next((ln for ln in buf.getvalue().splitlines() if ln.startswith("{")), None)
+        q.put((rank, json.loads(line) if line else None))
+    except Exception as e:  # surface worker failures to the parent
+        q.put((rank, repr(e)))
+
+
+def test_bench_two_ranks_rehearsal(dev):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(WORLD):
+        assert not isinstance(res[r], str), res[r]
+    d = res[0]
+    assert res[1] is None   # one JSON line, from rank 0
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 512 and d["value"] > 0
+    assert d["config"]["collective"]
