@@ -1,5 +1,7 @@
 """Per-launch duration and the gap before each launch, from a rocprofv3
-kernel-trace csv of tools/kbench.py (steady state: the last 100 forwards)."""
+kernel-trace csv of tools/kbench.py (steady state: the last 100 forwards) or
+of bench.py (argv: csv [first_forward count], e.g. 10 50 = timed region A of
+the default bench: 10 warm-up forwards, then 50 timed)."""
 import collections
 import csv
 import sys
@@ -19,7 +21,13 @@ def short(n):
 
 seq = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 per = len([s for s in seq if s[0] == "conv12"])
-start = len(seq) - 100 * 5
+if len(sys.argv) > 3:
+    first, count = int(sys.argv[2]), int(sys.argv[3])
+    c12 = [i for i, s in enumerate(seq) if s[0] == "conv12"]
+    start = c12[first]
+    seq = seq[:c12[first + count]] if first + count < len(c12) else seq
+else:
+    start = len(seq) - 100 * 5
 dur = collections.defaultdict(list)
 gap = collections.defaultdict(list)
 for i in range(max(start, 1), len(seq)):
