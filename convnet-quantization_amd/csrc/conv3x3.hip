@@ -431,6 +431,10 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // Same-box conv5+6 51.4 -> 47.9 us (profiles/r02_diag_stagger_step_ab.txt);
   // a whole-chunk stagger measured slower (r02_diag_stagger_chunk_ab.txt).
   const bool lag = C::NWAVES >= 8 && wave_u >= C::NWAVES / 2;
+  // the leading half issues first (s_setprio 1 for the loop): same-box
+  // conv5+6 48.0 -> 47.6 us; the lagging half at priority 1 measured 48.7
+  // (profiles/r02_diag_stagger_priority_ab.txt)
+  if (C::NWAVES >= 8 && !lag) __builtin_amdgcn_s_setprio(1);
   auto ring_barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -453,6 +457,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // every wave's last reads are consumed; the caller reuses the LDS
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
+  if (C::NWAVES >= 8) __builtin_amdgcn_s_setprio(0);
 }
 
 // Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
