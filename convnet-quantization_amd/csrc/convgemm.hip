@@ -26,14 +26,20 @@
 namespace qcn {
 
 // fp32(fp32(acc) + u*v) * mult for two channels (FBGEMM requant before the
-// rounding).  Scalar fma / mul (the build's -fno-slp-vectorize keeps them
-// scalar): packed fp32 issues slower beside a partner wave's MFMAs
-// (profiles/r01_diag_scalar_vs_packed_requant.txt).
+// rounding) as one packed fma and one packed mul: in these epilogue-bound
+// convs no MFMA stream competes with the packed issue (the SimpleConvNet ring
+// kernels keep scalar fp32 beside their partner waves' MFMAs).
 QCN_DEV v2f requant2(int a0, int a1, v2f u, v2f v, v2f m) {
-  float x = __builtin_fmaf(u.x, v.x, (float)a0), y = __builtin_fmaf(u.y, v.y, (float)a1);
-  x = x * m.x;
-  y = y * m.y;
-  return (v2f){x, y};
+  return __builtin_elementwise_fma(u, v, (v2f){(float)a0, (float)a1}) * m;
+}
+
+// floor(a / d) for 0 <= a < 2^22 and d >= 1 from an fp32 reciprocal estimate
+// (off by at most one) and one correction each way.
+QCN_DEV int div_small(int a, int d, float rd) {
+  int q = (int)((float)a * rd);
+  q -= (q * d > a) ? 1 : 0;
+  q += ((q + 1) * d <= a) ? 1 : 0;
+  return q;
 }
 
 
@@ -122,13 +128,25 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   long pbase[4];
   int iy0[4], ix0[4];
   bool pv[4];
+  // pixel -> (image, oy, ox): the tile's first pixel is split once (uniform;
+  // npix < 2^31 is checked at launch), each lane's offset (< 256) is carried
+  // through ox and oy with small fp32-reciprocal divisions — no 64-bit
+  // divisions per lane (they were ~half the VALU of the thin 1x1 convs)
+  const int ohw = a.oh * a.ow;
+  const int m0i = (int)m0;
+  const int img0 = m0i / ohw, rem0 = m0i - img0 * ohw;
+  const int oy00 = rem0 / a.ow, ox00 = rem0 - oy00 * a.ow;
+  const float rw = 1.0f / (float)a.ow, rh = 1.0f / (float)a.oh;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const long p = m0 + (wave + 4 * e) * 16 + (lane >> 2);
-    pv[e] = p < a.npix;
-    const long pc = pv[e] ? p : 0;
-    const int ox = (int)(pc % a.ow), oy = (int)((pc / a.ow) % a.oh);
-    const long img = pc / ((long)a.ow * a.oh);
+    const int off = (wave + 4 * e) * 16 + (lane >> 2);
+    pv[e] = m0 + off < a.npix;
+    const int tx = ox00 + off;
+    const int qx = div_small(tx, a.ow, rw);
+    const int ty = oy00 + qx;
+    const int qy = div_small(ty, a.oh, rh);
+    const int ox = tx - qx * a.ow, oy = ty - qy * a.oh;
+    const long img = pv[e] ? img0 + qy : 0;
     iy0[e] = oy * a.sy - a.py;
     ix0[e] = ox * a.sx - a.px;
     pbase[e] = ((img * a.h + iy0[e]) * a.w_ + ix0[e]) * (long)a.cin + bh * 16;
@@ -355,6 +373,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   // [BM][OS] (no lane transposes).
   const bool fast = a.zp_y == 0;
   const float zpf = (float)a.zp_y, lof = (float)a.lo;
+  const v2f zpv = {zpf, zpf};
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int cl = wc * 64 + i * 32;   // tile's first channel within the workgroup
@@ -384,6 +403,18 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
           wd = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g].y, 1, wd);
           wd = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g + 1].x, 2, wd);
           od[2 * g] = __builtin_amdgcn_cvt_pk_u8_f32(ab[2 * g + 1].y, 3, wd);
+        }
+      } else if (a.lo == 0) {
+        // clamp(rint + zp, 0, 255): v_cvt_pk_u8_f32 saturates to [0, 255] and
+        // rint + zp is integer-valued, so no med3
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const v2f r0 = (v2f){__builtin_rintf(ab[2 * g].x), __builtin_rintf(ab[2 * g].y)} + zpv;
+          const v2f r1 = (v2f){__builtin_rintf(ab[2 * g + 1].x), __builtin_rintf(ab[2 * g + 1].y)} + zpv;
+          uint32_t wd = __builtin_amdgcn_cvt_pk_u8_f32(r0.x, 0, 0u);
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(r0.y, 1, wd);
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(r1.x, 2, wd);
+          od[2 * g] = __builtin_amdgcn_cvt_pk_u8_f32(r1.y, 3, wd);
         }
       } else {
 #pragma unroll
@@ -462,6 +493,7 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   a.r = resid; a.s3 = y_scale; a.s_r = r_scale; a.inv_o = resid ? 1.0f / out_scale : 0.f;
   a.z_r = r_zp; a.z_o = out_zp; a.y = y;
   if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
+  if (a.npix >= (1L << 31) - 256) return QCN_ERR_UNSUPPORTED;   // 32-bit pixel indices in the kernel
   hipStream_t st = (hipStream_t)stream;
   if (cout % 128 == 0)
     return resid ? qcn::launch_gemm<128, true>(a, st) : qcn::launch_gemm<128, false>(a, st);
