@@ -9,7 +9,7 @@ import sys
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "qcn::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 names = {"conv12p": "conv12", "ConvCfg<64, 128": "conv34", "ConvCfg<128, 256": "conv56",
-         "fc_splitk": "fc_splitk", "fc_finish": "fc_finish"}
+         "fc_splitk": "fc_splitk", "fc_finish": "fc_finish", "fc_head_kernel": "fc_head"}
 
 
 def short(n):
@@ -35,7 +35,9 @@ for i in range(max(start, 1), len(seq)):
     dur[n].append((e - s) / 1e3)
     gap[n].append((s - seq[i - 1][2]) / 1e3)
 tot_d = tot_g = 0.0
-for n in ("conv12", "conv34", "conv56", "fc_splitk", "fc_finish"):
+for n in ("conv12", "conv34", "conv56", "fc_splitk", "fc_finish", "fc_head"):
+    if not dur[n]:
+        continue
     d = sum(dur[n]) / len(dur[n])
     g = sum(gap[n]) / len(gap[n])
     tot_d += d
