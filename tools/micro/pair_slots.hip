@@ -1,7 +1,7 @@
 // Diagnostic: where do the pair kernel's workgroups run (XCC / SE / CU /
 // workgroup slot, from HW_ID) and when, relative to their co-resident
-// partner?  Tests the lockstep hypothesis of DESIGN §5 and the first-round
-// lead sleep (QCN_PAIR_SLEEP).  Build + run on the box (repo root):
+// partner?  Tests the lockstep hypothesis of DESIGN §5 (the lead-sleep knob
+// QCN_PAIR_SLEEP it was first run with is gone from the kernel).  Build + run on the box (repo root):
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -DQCN_STAMPS \
 //     -Iinclude -Iconvnet-quantization_amd/csrc tools/micro/pair_slots.hip -o /tmp/pair_slots
 //   QCN_PAIR_SLEEP=8 /tmp/pair_slots 64    (64: conv3+conv4; 128: conv5+conv6)
