@@ -196,9 +196,34 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < C::JT; ++j) acc[i][j] = c0;
   }
+  // Residual join (RESID): the identity bytes each thread's phase-2 rows need
+  // (constant row set per thread, see the epilogue).  With at most two stages
+  // (conv3 with K <= 128) they are loaded right behind the stage DMAs, so
+  // their HBM latency overlaps the DMA wait and the MFMAs instead of following
+  // them; longer K loads them before the requant phase.  Rows past npix load
+  // the last pixel's bytes (unused) so every wave issues the same count.
+  constexpr int R_NCOL = 32 * C::WN;           // local columns per channel half
+  constexpr int R_TPR = R_NCOL / 16, R_RPI = 256 / R_TPR, NIT = C::BM / R_RPI;
+  const int rr = tid / R_TPR, cq = tid % R_TPR;   // phase-2 row / 16-column group
+  const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i
+  uint4 rid[2][NIT];
+  auto load_id = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        long pp = m0 + it * R_RPI + rr;
+        pp = pp < a.npix ? pp : a.npix - 1;
+        rid[i][it] = *reinterpret_cast<const uint4*>(a.r + pp * a.cout + ch2 + 32 * i);
+      }
+  };
+  const bool early = RESID && nst <= 2;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   issue(0);
   if (nst > 1) issue(1);
+  if constexpr (RESID) {
+    if (early) load_id();
+  }
 
   // MFMA read offsets: A lane-linear; B row (wm*JT + j)*32 + l32, piece 2c+hi
   const int swz = (l32 >> 2) & 3;
@@ -235,8 +260,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     }
   };
   v4i fa0[2], fb0[C::JT], fa1[2], fb1[C::JT];
-  if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (early identity loads are the youngest 2 * NIT vector-memory operations)
+  if (early) {
+    if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D + 2 * NIT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIT) : "memory");
+  } else {
+    if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -249,7 +280,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     const bool more = st + 1 < nst;
     if (more) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage st+1 (the only DMA in flight)
+      // stage st+1 (the only DMA in flight; behind it only early identity loads)
+      if (early) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (st + 2 < nst) issue(st + 2);
@@ -268,26 +301,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     // exactly (conv3 has no ReLU), so the u8 y3 is never materialised — into
     // an LDS tile [BM][32*WN floats]; phase 2 reads it row-contiguous next to
     // the coalesced identity bytes: out = quantize(relu(d3 + s_r*(r - z_r))).
-    constexpr int NCOL = 32 * C::WN;           // local columns per half
-    constexpr int OSF = NCOL * 4 + 16;         // fp32 row stride (bytes)
-    constexpr int TPR = NCOL / 16, RPI = 256 / TPR;
+    constexpr int OSF = R_NCOL * 4 + 16;       // fp32 row stride (bytes)
+    constexpr int RPI = R_RPI;
     static_assert(C::BM * OSF <= C::LDS, "fp32 staging fits in the ring");
     const v2f nz3 = {-(float)a.zp_y, -(float)a.zp_y}, hz3 = {255.0f - a.zp_y, 255.0f - a.zp_y};
     const v2f s3 = {a.s3, a.s3};
-    const int rr = tid / TPR, cq = tid % TPR;   // phase-2 row / 16-column group
-    const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i
-    // the identity bytes of both halves' phase 2, loaded before phase 1 so
-    // their HBM latency hides behind the requant math (rows past npix: 0)
-    constexpr int NIT = C::BM / RPI;
-    uint4 rid[2][NIT];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const long p = m0 + it * RPI + rr;
-        rid[i][it] = p < a.npix ? *reinterpret_cast<const uint4*>(a.r + p * a.cout + ch2 + 32 * i)
-                                : make_uint4(0u, 0u, 0u, 0u);
-      }
+    // longer K: the identity bytes of both halves' phase 2, loaded before
+    // phase 1 so their HBM latency hides behind the requant math
+    if (!early) load_id();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int co0 = n0 + wc * 64 + i * 32;
@@ -437,10 +458,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   // segments per store instruction.
   constexpr int TPR = BN / 16;            // threads per row
   constexpr int RPI = 256 / TPR;          // rows per iteration
-  const int rr = tid / TPR, cc = (tid % TPR) * 16;
+  const int orr = tid / TPR, cc = (tid % TPR) * 16;
 #pragma unroll 2
   for (int r0 = 0; r0 < C::BM; r0 += RPI) {
-    const int row = r0 + rr;
+    const int row = r0 + orr;
     const long p = m0 + row;
     if (p >= a.npix) break;
     *reinterpret_cast<uint4*>(a.y + p * a.cout + n0 + cc) =
