@@ -356,6 +356,10 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the forward as one HIP graph (measured: no gain, the launch "
                          "queue already runs back to back)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="resnet50: split the batch over this many HIP streams, launches "
+                         "interleaved layer by layer (QuantizedResNet.run_streams; measured "
+                         "1/2/3/4: 81.7/86.7/86.3/72.1 K img/s at batch 512)")
     ap.add_argument("--workload", choices=("convnet", "qdq", "resnet50"), default="convnet",
                     help="convnet: BASELINE configs[2]/[3] (the metric); qdq: configs[1] (per-layer "
                          "QDQ CustomQuantizationModel, batch 256); resnet50: configs[4]")
@@ -559,6 +563,8 @@ def main_resnet(args):
     def step(marks=None):
         if marks is None and use_graph:
             logits = model.replay(B)
+        elif marks is None and args.streams > 1:
+            logits = model.run_streams(x, args.streams)
         else:
             logits = model.run(x, marks=marks)
         if world > 1:
@@ -624,7 +630,7 @@ def main_resnet(args):
         "config": {"workload": "ResNet-50 (stem, 16 bottleneck blocks, avgpool, fc) static int8, "
                                "per-channel weights, u8 NHWC activations",
                    "global_batch": world * B, "per_gpu_batch": B, "image": [3, 224, 224],
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "streams": args.streams},
         "roofline": roof,
         "launch_ms": {k: round(float(np.sum(v) / n_rep), 4) for k, v in per_name.items()},
         "conv_gmac_per_image": sum(mac_img) / 1e9,

@@ -228,6 +228,47 @@ class QuantizedResNet:
             return self._run(x, keep, marks)
 
     def _run(self, x, keep, marks):
+        g = self._steps(x, keep, marks)
+        while True:
+            try:
+                next(g)
+            except StopIteration as e:
+                return e.value
+
+    def run_streams(self, x, nsplit=2):
+        """The forward over `nsplit` slices of the batch, each on its own HIP
+        stream, launches interleaved layer by layer: one slice's layer tail
+        (its last, partly filled round of workgroups) runs beside the other
+        slice's layer instead of leaving CUs idle.  Ordered after the current
+        stream's prior work; the current stream waits for the result."""
+        if x.device != self.device:
+            raise ValueError(f"input on {x.device}, model on {self.device}")
+        with torch.cuda.device(self.device):
+            main = torch.cuda.current_stream(self.device)
+            if len(getattr(self, "_side", ())) < nsplit:
+                self._side = [torch.cuda.Stream(device=self.device) for _ in range(nsplit)]
+            streams = self._side[:nsplit]
+            for s in streams:
+                s.wait_stream(main)
+            gens = [self._steps(c, False, None) for c in x.chunk(nsplit)]
+            outs = [None] * len(gens)
+            live = list(range(len(gens)))
+            while live:
+                for i in list(live):
+                    with torch.cuda.stream(streams[i]):
+                        try:
+                            next(gens[i])
+                        except StopIteration as e:
+                            outs[i] = e.value
+                            live.remove(i)
+            for s in streams:
+                main.wait_stream(s)
+            for o, s in zip(outs, streams):
+                o.record_stream(main)   # allocated on a side stream, read on main
+            return torch.cat(outs)
+
+    def _steps(self, x, keep, marks):
+        """The forward as a generator: one yield after each launch."""
         inter = {}
 
         def mark(name):
@@ -240,10 +281,13 @@ class QuantizedResNet:
         mark("start")
         q = ops.stem_pack(x, self.in_scale, self.in_zp)
         mark("stem_pack")
+        yield
         q = ops.conv(q, self.in_zp, self.stem)
         mark("conv")
+        yield
         q = ops.maxpool3x3s2(q)
         mark("maxpool")
+        yield
         if keep:
             inter["stem"] = q
         fuse = os.environ.get("QCN_RESID_FUSED", "1") == "1"
@@ -252,27 +296,33 @@ class QuantizedResNet:
             if b["ds"] is not None:   # identity first, so conv3 can consume it
                 idn = ops.conv(q, zx, b["ds"])
                 mark("conv")
+                yield
                 si, zi = e["ds"]["s_y"], e["ds"]["z_y"]
             else:
                 idn, si, zi = q, e["c1"]["s_x"], zx
             y = ops.conv(q, zx, b["c1"])
             mark("conv")
+            yield
             y = ops.conv(y, b["c2"].z_x, b["c2"])
             mark("conv")
+            yield
             so, zo = e["out"]
             if fuse:   # conv3 + residual join in one launch
                 q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
                 mark("conv")
+                yield
             else:
                 y = ops.conv(y, b["c3"].z_x, b["c3"])
                 mark("conv")
                 q = ops.add_relu(y, e["c3"]["s_y"], e["c3"]["z_y"], idn, si, zi, so, zo, True)
                 mark("add")
+                yield
             if keep:
                 inter[f"block{i}"] = q
         last = sp["blocks"][-1]["out"] if sp["blocks"] else (sp["stem"]["s_y"], sp["stem"]["z_y"])
         q = ops.avgpool(q, last[1])   # qparams kept: the fc reads `last`'s qparams
         mark("avgpool")
+        yield
         if keep:
             inter["pool"] = q
         f = self.fc
@@ -303,7 +353,9 @@ class QuantizedResNet:
     def forward(self, x):
         host = not x.is_cuda
         xd = x.to(self.device, torch.float32).contiguous()
-        out = self.run(xd).clone()
+        # two interleaved stream slices fill each layer's last workgroup round
+        # (+6 % at batch 512, profiles/r02_diag_resnet_streams.txt)
+        out = self.run_streams(xd, 2) if xd.shape[0] >= 128 else self.run(xd).clone()
         if host or self.host_io:
             return out.cpu()
         torch.cuda.current_stream(self.device).synchronize()

@@ -187,6 +187,21 @@ def test_resnet_bit_exact(dev, layers, hw, n):
     assert rel < 0.35, rel
 
 
+@pytest.mark.parametrize("nsplit", [2, 3])
+def test_resnet_run_streams_equals_run(dev, nsplit):
+    """run_streams (batch slices on their own HIP streams, launches interleaved
+    layer by layer) gives the one-stream logits bit for bit, also for a batch
+    that does not split evenly."""
+    from models.resnet import synthetic_images
+    _, qm = _net(dev, (1, 1, 1, 1), 64, 0)
+    x = torch.from_numpy(synthetic_images(7, 5, 64)).to(dev)
+    ref = qm.run(x).clone()
+    for _ in range(2):   # second pass: side streams reused
+        out = qm.run_streams(x, nsplit)
+        assert torch.equal(out, ref)
+    torch.cuda.synchronize()
+
+
 def test_resnet_equals_torchao_fixture(dev):
     """§8(f)2 whole-net pin on the GPU: the 1-1-1-1 bottleneck ResNet at 64x64
     with torch.ao's qparams (tests/golden/net_resnet_int8.npz) — stem, every
