@@ -73,6 +73,8 @@ SIGNATURES = {
     "qcn_classifier_qdq_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, f32, vp, i32, vp,
                                       vp, vp, vp, vp]),
     "qcn_pack_conv_weight_kmajor": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "qcn_resnet_stem_fused": (i32, [vp, i32, i32, i32, f32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
+                                    vp, vp]),
     "qcn_conv_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
                                  vp, vp, vp, vp, i32, i32, vp, vp]),
     "qcn_conv_gemm_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32,

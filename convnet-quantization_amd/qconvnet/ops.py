@@ -434,6 +434,23 @@ def stem_pack(x, scale, zp, out=None):
     return out
 
 
+def stem_fused(x, scale, zp, layer, out=None):
+    """QuantStub -> 7x7/2 stem conv (+ReLU requant) -> 3x3/2 max-pool in one
+    launch (qcn_resnet_stem_fused); ``layer`` as for conv() with the weights
+    packed from stem_weight_rows.  Input [n,3,s,s] fp32, s in {224, 64}."""
+    _need(x, torch.float32, "stem.x")
+    n, c, h, w = x.shape
+    d = layer
+    if c != 3 or h != w or d.cout != 64:
+        raise ValueError("stem_fused: 3-channel square input, 64 output channels")
+    if out is None:
+        out = torch.empty((n, h // 4, w // 4, 64), dtype=torch.uint8, device=x.device)
+    check(lib().qcn_resnet_stem_fused(_ptr(x), n, h, w, float(scale), int(zp), _ptr(d.w), d.cout,
+                                      _ptr(d.u), _ptr(d.v), _ptr(d.mult), _ptr(d.corr), int(d.z_y),
+                                      int(bool(d.relu)), _ptr(out), _stream()), "stem_fused")
+    return out
+
+
 def avgpool(x, x_zp, out=None):
     """Global average pool of u8 NHWC [n,h,w,c] -> [n,c], qparams kept
     (torch's quantized adaptive_avg_pool2d)."""

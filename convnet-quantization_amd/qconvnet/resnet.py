@@ -212,6 +212,16 @@ class QuantizedResNet:
         self.fc = d
         self.num_classes = w.shape[0]
 
+    def _stem_fusable(self, x):
+        """The one-launch stem (qcn_resnet_stem_fused) covers torchvision's
+        7x7/2 pad-3 64-channel stem at 224x224 and 64x64 inputs;
+        QCN_STEM_FUSED=0 selects the three-launch form."""
+        e = self.spec["stem"]
+        return (os.environ.get("QCN_STEM_FUSED", "1") == "1" and self.stem.cout == 64
+                and tuple(np.asarray(e["w"]).shape[1:]) == (3, 7, 7)
+                and tuple(e["stride"]) == (2, 2) and tuple(e["pad"]) == (3, 3)
+                and x.shape[1] == 3 and x.shape[2] == x.shape[3] and x.shape[2] in (224, 64))
+
     def conv_layers(self):
         """Every conv launch in forward order (for MAC accounting)."""
         out = [self.stem]
@@ -279,15 +289,20 @@ class QuantizedResNet:
 
         sp = self.spec
         mark("start")
-        q = ops.stem_pack(x, self.in_scale, self.in_zp)
-        mark("stem_pack")
-        yield
-        q = ops.conv(q, self.in_zp, self.stem)
-        mark("conv")
-        yield
-        q = ops.maxpool3x3s2(q)
-        mark("maxpool")
-        yield
+        if self._stem_fusable(x):   # quantize + conv + ReLU + max-pool in one launch
+            q = ops.stem_fused(x, self.in_scale, self.in_zp, self.stem)
+            mark("conv")   # carries the stem MACs (bench / resnet_layers accounting)
+            yield
+        else:
+            q = ops.stem_pack(x, self.in_scale, self.in_zp)
+            mark("stem_pack")
+            yield
+            q = ops.conv(q, self.in_zp, self.stem)
+            mark("conv")
+            yield
+            q = ops.maxpool3x3s2(q)
+            mark("maxpool")
+            yield
         if keep:
             inter["stem"] = q
         fuse = os.environ.get("QCN_RESID_FUSED", "1") == "1"

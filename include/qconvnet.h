@@ -260,6 +260,18 @@ int qcn_maxpool3x3s2_u8_nhwc(const uint8_t* x, int nimg, int h, int w, int c, ui
  * zero point outside the image and in bytes 21..31.  ow = (w-1)/2 + 1. */
 int qcn_stem_pack_f32_nchw(const float* x, int nimg, int h, int w, float scale, int zp, uint8_t* y,
                            void* stream);
+/* The whole ResNet stem in one launch: QuantStub (scale, zp) on fp32 NCHW
+ * [n][3][h][w] -> 7x7/2 pad-3 conv 3->64 (w_packed = stem_weight_rows packed
+ * k-major, [7][64][32]; u/v/mult/corr and y_zp/relu as qcn_conv_gemm_u8s8_nhwc)
+ * -> MaxPool2d(3, 2, padding=1) -> u8 NHWC [n][h/4][w/4][64].  Bit-identical
+ * to qcn_stem_pack_f32_nchw + qcn_conv_gemm_u8s8_nhwc (7x1, strides (2,1), pad
+ * (3,0)) + qcn_maxpool3x3s2_u8_nhwc; replaces the reference's
+ * conv1/bn1/relu/maxpool of custom_quantization_model.py:117-141 after its
+ * QuantStub.  h == w in {224, 64}, cout == 64, else QCN_ERR_UNSUPPORTED. */
+int qcn_resnet_stem_fused(const float* x, int nimg, int h, int w, float scale, int zp,
+                          const int8_t* w_packed, int cout, const float* u, const float* v,
+                          const float* mult, const int32_t* corr, int y_zp, int relu, uint8_t* y,
+                          void* stream);
 /* AdaptiveAvgPool2d(1) on u8 NHWC [nimg][hw][c] -> [nimg][c], quantization
  * parameters kept (torch's quantized adaptive_avg_pool2d, the avgpool of a
  * static-int8 ResNet ahead of its fc): y = clamp(x_zp + rne(fp32(sum_q -

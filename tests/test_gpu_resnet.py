@@ -187,6 +187,29 @@ def test_resnet_bit_exact(dev, layers, hw, n):
     assert rel < 0.35, rel
 
 
+@pytest.mark.parametrize("hw,n,per_channel", [(224, 3, True), (64, 5, True), (64, 4, False)])
+def test_stem_fused_equals_three_launches(dev, hw, n, per_channel):
+    """qcn_resnet_stem_fused (quantize + 7x7/2 conv + ReLU + 3x3/2 max-pool in
+    one launch) equals stem_pack -> 7x1 conv_gemm -> maxpool3x3s2 byte for
+    byte, with inputs past the quantization range on both sides (clamps) and
+    images whose last band ends at the border."""
+    from models.resnet import synthetic_images, synthetic_resnet
+    from qconvnet import ops
+    from qconvnet.resnet import quantize_resnet
+    m = synthetic_resnet(3, (1, 1, 1, 1), num_classes=10, hw=hw, calib_images=4, device=dev)
+    qm = quantize_resnet(m, [torch.from_numpy(synthetic_images(4, 13, hw))], dev,
+                         per_channel=per_channel)
+    x = torch.from_numpy(synthetic_images(n, 17, hw)).to(dev)
+    x[0, :, :3, :5] = 50.0     # past the top of the range
+    x[-1, 1, -4:, -3:] = -50.0  # past the bottom
+    assert qm._stem_fusable(x)
+    ref = ops.maxpool3x3s2(ops.conv(ops.stem_pack(x, qm.in_scale, qm.in_zp), qm.in_zp, qm.stem))
+    got = ops.stem_fused(x, qm.in_scale, qm.in_zp, qm.stem)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (n, hw // 4, hw // 4, 64)
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("nsplit", [2, 3])
 def test_resnet_run_streams_equals_run(dev, nsplit):
     """run_streams (batch slices on their own HIP streams, launches interleaved
