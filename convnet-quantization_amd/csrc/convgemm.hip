@@ -75,17 +75,20 @@ struct GemmArgs {
 template <int BN>
 struct GemmCfg {
   static constexpr int BM = 256;
+  static constexpr int NW = BN == 256 ? 8 : 4;   // waves (BN = 256: 512 threads, one per CU)
+  static constexpr int NT = 64 * NW;
   static constexpr int WN = BN / 64;          // waves along channels
-  static constexpr int WM = 4 / WN;           // waves along pixels
+  static constexpr int WM = NW / WN;          // waves along pixels
   static constexpr int JT = BM / (32 * WM);   // pixel tiles per wave (4 or 2)
   static constexpr int FA = 2 * BN / 32;      // A fragments (1 KiB) per stage
   static constexpr int AREG = FA * 1024;      // A region of a stage
   static constexpr int STAGE = AREG + BM * 64;
-  static constexpr int DA = FA / 4;           // A DMA instructions per wave per stage
-  static constexpr int D = DA + 4;            // + 4 B instructions (16 rows x 64 B each)
+  static constexpr int DA = FA / NW;          // A DMA instructions per wave per stage
+  static constexpr int NB = BM * 64 / 1024 / NW;   // B DMA instructions (16 rows x 64 B) per wave
+  static constexpr int D = DA + NB;
   static constexpr int OS = BN + 16;          // output staging row stride (bytes)
   static constexpr int LDS = 3 * STAGE;
-  static_assert(FA % 4 == 0, "A fragments split evenly over 4 waves");
+  static_assert(FA % NW == 0, "A fragments split evenly over the waves");
   static_assert(BM * OS <= LDS, "output staging fits in the ring");
 };
 
@@ -102,7 +105,7 @@ struct KCursor {
 };
 
 template <int BN, bool RESID>
-__global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
+__global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_gemm_kernel(GemmArgs a) {
   using C = GemmCfg<BN>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -125,9 +128,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   // so every lane loads the same piece (chunk c, half h) of its 4 rows.
   const int bslot = lane & 3, bswz = (lane >> 4) & 3, bpc = bslot ^ bswz;
   const int bc = bpc >> 1, bh = bpc & 1;
-  long pbase[4];
-  int iy0[4], ix0[4];
-  bool pv[4];
+  long pbase[C::NB];
+  int iy0[C::NB], ix0[C::NB];
+  bool pv[C::NB];
   // pixel -> (image, oy, ox): the tile's first pixel is split once (uniform;
   // npix < 2^31 is checked at launch), each lane's offset (< 256) is carried
   // through ox and oy with small fp32-reciprocal divisions — no 64-bit
@@ -138,8 +141,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   const int oy00 = rem0 / a.ow, ox00 = rem0 - oy00 * a.ow;
   const float rw = 1.0f / (float)a.ow, rh = 1.0f / (float)a.oh;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int off = (wave + 4 * e) * 16 + (lane >> 2);
+  for (int e = 0; e < C::NB; ++e) {
+    const int off = (wave + C::NW * e) * 16 + (lane >> 2);
     pv[e] = m0 + off < a.npix;
     const int tx = ox00 + off;
     const int qx = div_small(tx, a.ow, rw);
@@ -163,8 +166,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   auto issue = [&](int st) {
     uint8_t* buf = lds + (st % 3) * C::STAGE;
 #pragma unroll
-    for (int tt = 0; tt < C::DA; ++tt) {   // A: fragment f = wave + 4 tt
-      const int f = wave + 4 * tt, c = f / (BN / 32), g = f % (BN / 32);
+    for (int tt = 0; tt < C::DA; ++tt) {   // A: fragment f = wave + NW tt
+      const int f = wave + C::NW * tt, c = f / (BN / 32), g = f % (BN / 32);
       const int kc = 2 * st + c;
       const void* src = kc < a.kcs ? (const void*)(wl + kc * wstep + g * 32 * 32) : (const void*)zero;
       glds16(src, buf + f * 1024);
@@ -173,11 +176,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     const bool live = 2 * st + bc < a.kcs;
     const long toff = ((long)lr * a.w_ + ls) * a.cin + lc;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {          // B: instruction wave + 4 e
+    for (int e = 0; e < C::NB; ++e) {      // B: instruction wave + NW e
       const int iy = iy0[e] + lr, ix = ix0[e] + ls;
       const bool in = live && pv[e] && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w_;
       const void* src = in ? (const void*)(a.x + pbase[e] + toff) : (const void*)zpl;
-      glds16(src, buf + C::AREG + (wave + 4 * e) * 1024);
+      glds16(src, buf + C::AREG + (wave + C::NW * e) * 1024);
     }
     cur0.adv(a.cin, a.kw); cur0.adv(a.cin, a.kw);
     cur1.adv(a.cin, a.kw); cur1.adv(a.cin, a.kw);
@@ -202,19 +205,24 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   // their HBM latency overlaps the DMA wait and the MFMAs instead of following
   // them; longer K loads them before the requant phase.  Rows past npix load
   // the last pixel's bytes (unused) so every wave issues the same count.
-  constexpr int R_NCOL = 32 * C::WN;           // local columns per channel half
-  constexpr int R_TPR = R_NCOL / 16, R_RPI = 256 / R_TPR, NIT = C::BM / R_RPI;
+  // The join runs in passes p = (channel half i, wave-column pair h): the
+  // waves of columns 2h, 2h + 1 stage their 32-channel half i, R_NCOL columns.
+  constexpr int NSUB = C::WN > 2 ? C::WN / 2 : 1, NPASS = 2 * NSUB;
+  constexpr int R_NCOL = 32 * (C::WN < 2 ? C::WN : 2);   // staged columns per pass
+  constexpr int R_TPR = R_NCOL / 16, R_RPI = C::NT / R_TPR, NIT = C::BM / R_RPI;
+  constexpr int NIDL = NPASS * NIT;            // identity loads per thread
   const int rr = tid / R_TPR, cq = tid % R_TPR;   // phase-2 row / 16-column group
-  const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i
-  uint4 rid[2][NIT];
+  const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i + 128 h
+  uint4 rid[NPASS][NIT];
   auto load_id = [&]() {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int p = 0; p < NPASS; ++p)
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         long pp = m0 + it * R_RPI + rr;
         pp = pp < a.npix ? pp : a.npix - 1;
-        rid[i][it] = *reinterpret_cast<const uint4*>(a.r + pp * a.cout + ch2 + 32 * i);
+        rid[p][it] = *reinterpret_cast<const uint4*>(a.r + pp * a.cout + ch2 + 32 * (p / NSUB) +
+                                                     128 * (p % NSUB));
       }
   };
   const bool early = RESID && nst <= 2;
@@ -260,10 +268,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     }
   };
   v4i fa0[2], fb0[C::JT], fa1[2], fb1[C::JT];
-  // (early identity loads are the youngest 2 * NIT vector-memory operations)
+  // (early identity loads are the youngest NIDL vector-memory operations)
   if (early) {
-    if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D + 2 * NIT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIT) : "memory");
+    if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D + NIDL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIDL) : "memory");
   } else {
     if (nst > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::D) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     const bool more = st + 1 < nst;
     if (more) {
       // stage st+1 (the only DMA in flight; behind it only early identity loads)
-      if (early) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NIT) : "memory");
+      if (early) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NIDL) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -310,7 +318,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
     // phase 1 so their HBM latency hides behind the requant math
     if (!early) load_id();
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int p = 0; p < NPASS; ++p) {
+      const int i = p / NSUB, hsub = p % NSUB;
       const int co0 = n0 + wc * 64 + i * 32;
       v2f u[8], v[8], mu[8];
 #pragma unroll
@@ -325,7 +334,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < C::JT; ++j) {
-        uint8_t* rowp = lds + ((wm * C::JT + j) * 32 + l32) * OSF + (wc * 32) * 4;
+        if (NSUB > 1 && (wc >> 1) != hsub) break;   // another pass's columns
+        uint8_t* rowp = lds + ((wm * C::JT + j) * 32 + l32) * OSF + ((wc & 1) * 32) * 4;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           v2f d[2];
@@ -347,10 +357,10 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
           const int row = it * RPI + rr;
-          const long p = m0 + row;
-          if (p >= a.npix) break;
-          const long off = p * a.cout + ch2 + 32 * i;
-          const uint4 rv = rid[i][it];
+          const long px = m0 + row;
+          if (px >= a.npix) break;
+          const long off = px * a.cout + ch2 + 32 * i + 128 * hsub;
+          const uint4 rv = rid[p][it];
           const float4* dp = reinterpret_cast<const float4*>(lds + row * OSF + cq * 64);
           const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
           uint32_t ow[4];
@@ -457,7 +467,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(GemmArgs a) {
   // Epilogue phase 2 (row-contiguous): 16 B per thread, whole 64/128-B row
   // segments per store instruction.
   constexpr int TPR = BN / 16;            // threads per row
-  constexpr int RPI = 256 / TPR;          // rows per iteration
+  constexpr int RPI = C::NT / TPR;        // rows per iteration
   const int orr = tid / TPR, cc = (tid % TPR) * 16;
 #pragma unroll 2
   for (int r0 = 0; r0 < C::BM; r0 += RPI) {
@@ -477,7 +487,7 @@ int launch_gemm(GemmArgs& a, hipStream_t st) {
   static bool attr_done[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)conv_gemm_kernel<BN, RESID>, C::LDS, attr_done))
     return QCN_ERR_HIP;
-  hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID>), dim3(a.mt * a.nt), dim3(256), C::LDS, st, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID>), dim3(a.mt * a.nt), dim3(C::NT), C::LDS, st, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
@@ -516,6 +526,12 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
   if (a.npix >= (1L << 31) - 256) return QCN_ERR_UNSUPPORTED;   // 32-bit pixel indices in the kernel
   hipStream_t st = (hipStream_t)stream;
+  // 256-channel tiles (8 waves; every gathered B row serves 256 output
+  // channels) where they measured faster: the 3x3 convs and the deepest 1x1
+  // (-5..8 %); the residual-join convs lose 30-40 % at one workgroup per CU
+  // (profiles/r02_diag_resnet_bn256_layers.txt)
+  if (cout % 256 == 0 && !resid && (kh * kw > 1 || cin >= 2048))
+    return qcn::launch_gemm<256, false>(a, st);
   if (cout % 128 == 0)
     return resid ? qcn::launch_gemm<128, true>(a, st) : qcn::launch_gemm<128, false>(a, st);
   return resid ? qcn::launch_gemm<64, true>(a, st) : qcn::launch_gemm<64, false>(a, st);
