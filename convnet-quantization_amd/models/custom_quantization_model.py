@@ -21,14 +21,20 @@ torch.ao's fp32 op order, so the integer chain is bit-exact with torch.ao
 from __future__ import annotations
 
 import torch
+import torch.nn as nn
 
 from models.baseline_model import SimpleConvNet, load_checkpoint_state
 from qconvnet import data
 from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
 
 
-class CustomQuantizationModel:
+class CustomQuantizationModel(nn.Module):
+    """An nn.Module like the reference's (:145): ``model`` (the fp32
+    SimpleConvNet) is its submodule, so state_dict() / parameters() / train()
+    / eval() behave as there; ``quantized_model`` is the MI355X executor."""
+
     def __init__(self, device="cuda"):
+        super().__init__()
         self.model = SimpleConvNet()
         self.quantized_model = None
         self.is_custom_quantized = True
@@ -59,16 +65,9 @@ class CustomQuantizationModel:
             return self.quantized_model(x)
         return self.model(x)
 
-    def __call__(self, x):
-        return self.forward(x)
-
-    def eval(self):
-        self.model.eval()
-        return self
-
     def to(self, device):
         if self.quantized_model is not None:
-            self.quantized_model.to(device)
+            self.quantized_model.to(device)   # compute stays on the GPU; host I/O
         else:
             self.model.to(device)
         return self
@@ -76,11 +75,8 @@ class CustomQuantizationModel:
     def cpu(self):
         return self.to("cpu")
 
-    def state_dict(self):
-        return self.model.state_dict()
 
-
-class CustomQuantizedResNet50:
+class CustomQuantizedResNet50(nn.Module):
     """Drop-in for CustomQuantizedResNet50
     (/root/reference/models/custom_quantization_model.py:104-148): wraps a
     torchvision-layout ResNet (models.resnet.resnet50 or a torchvision model) —
@@ -105,6 +101,7 @@ class CustomQuantizedResNet50:
         from models.resnet import synthetic_images
         if mode not in ("static", "reference"):
             raise ValueError(f"unknown mode {mode!r}")
+        super().__init__()
         if calibration_batches is None:
             calibration_batches = [torch.from_numpy(synthetic_images(32, 1))]
         batches = [b[0] if isinstance(b, (tuple, list)) else b for b in calibration_batches]
@@ -113,13 +110,13 @@ class CustomQuantizedResNet50:
         build = quantize_resnet if mode == "static" else quantize_resnet_reference
         self.quantized_model = build(model.eval(), batches, device, per_channel)
 
-    def __call__(self, x):
+    def forward(self, x):
         return self.quantized_model(x)
 
-    forward = __call__
-
-    def eval(self):
-        return self
+    def train(self, mode=True):
+        if mode:
+            raise RuntimeError("CustomQuantizedResNet50 is inference-only")
+        return super().train(False)
 
     def to(self, device):
         self.quantized_model.to(device)

@@ -104,3 +104,25 @@ def test_model_evaluator_matches_numpy_topk():
         assert abs(got[k] - v) < 1e-9
     res = ev.compare_models({"m": _FixedLogits(torch.from_numpy(logits), bs)}, classes)
     assert abs(res["m"]["accuracy"] - 100.0 * (pred == labels).sum() / n) < 1e-9
+
+
+def test_custom_quantization_model_is_an_nn_module():
+    """CustomQuantizationModel is an nn.Module with the fp32 SimpleConvNet as
+    its `model` submodule, like the reference's (custom_quantization_model.py:
+    145-151): state_dict keys carry the `model.` prefix, load_state_dict takes
+    a bare SimpleConvNet state dict (:163-167), and before quantize() the
+    forward is the fp32 net (:196-199)."""
+    import torch
+    from models.baseline_model import SimpleConvNet
+    from models.custom_quantization_model import CustomQuantizationModel
+    m = CustomQuantizationModel()
+    assert isinstance(m, torch.nn.Module)
+    keys = set(m.state_dict())
+    assert {"model.conv1.weight", "model.bn7.running_var", "model.fc2.bias"} <= keys
+    ref = SimpleConvNet().eval()
+    m.load_state_dict(ref.state_dict())
+    m.eval()
+    assert not m.model.training
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        assert torch.equal(m(x), ref(x))
