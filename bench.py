@@ -382,19 +382,39 @@ def main():
     model, sd = build_model(rank, dev, args.per_channel, args.spec_file, mode)
     B = args.batch
     x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
-    gathered = torch.empty((world * B, 10), dtype=torch.float32, device=dev) if world > 1 else None
+    # N > 1: the logits all-gather of batch k runs while batch k+1 is computed
+    # (two logits buffers, model slots k % 2; the gather of batch k is waited
+    # for before slot k % 2 is reused, and all of them before the clock stops)
+    gathered = [torch.empty((world * B, 10), dtype=torch.float32, device=dev)
+                for _ in range(2)] if world > 1 else None
+    pending = [None, None]
+    nstep = [0]
 
     use_graph = args.graph
     if use_graph:   # the forward's launches as one HIP graph (same kernels, no launch gaps)
         model.capture_graph(x)
 
     def step(marks=None):
+        slot = nstep[0] % 2 if world > 1 else 0
+        if pending[slot] is not None:
+            pending[slot].wait()
+            pending[slot] = None
         if marks is None and use_graph:
             logits = model.replay(B)
         else:
-            logits = model.run(x, marks=marks)
+            logits = model.run(x, marks=marks, slot=slot)
         if world > 1:
-            qd.gather_logits(logits, gathered)
+            pending[slot] = qd.gather_logits_async(logits, gathered[slot])
+            if use_graph:   # the graph has one logits buffer: done before the next replay
+                pending[slot].wait()
+                pending[slot] = None
+        nstep[0] += 1
+
+    def drain():   # every outstanding all-gather has completed on the current stream
+        for i in range(2):
+            if pending[i] is not None:
+                pending[i].wait()
+                pending[i] = None
 
     def barrier():
         if world > 1:
@@ -402,6 +422,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
 
     # ---- timed region A: the metric
@@ -410,6 +431,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -428,6 +450,7 @@ def main():
         m = []
         step(m)
         marks_all.append(m)
+    drain()
     torch.cuda.synchronize()
     names = model.kernel_names(x.shape)
     per = {n: [] for n in names}

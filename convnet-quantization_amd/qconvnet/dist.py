@@ -67,6 +67,17 @@ def gather_logits(local, out=None):
     return out
 
 
+def gather_logits_async(local, out):
+    """gather_logits without blocking: the all-gather is enqueued behind the
+    current stream's work (RCCL runs it on its own stream) and the current
+    stream only waits for it at ``work.wait()``, so the next batch's forward
+    overlaps it (its logits must go to another buffer meanwhile).  Returns
+    the work handle, or None at world size 1."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return None
+    return dist.all_gather_into_tensor(out, local.contiguous(), async_op=True)
+
+
 def global_minmax(mm):
     """All-reduce a [min, max] pair over the ranks (one 2-float collective:
     MIN over [min, -max]; negation is exact).  This is the exchange that makes

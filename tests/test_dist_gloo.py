@@ -45,6 +45,14 @@ def _worker(rank, world, port, q):
             return torch.from_numpy(qref.static_int8_forward(xs.numpy(), qm)[0])
 
         out = qd.sharded_forward(model_fn, x)
+        # bench.py's N > 1 loop: two batches' all-gathers in flight at once
+        s, e = qd.shard(x.shape[0], world, rank)
+        bufs = [torch.empty_like(out), torch.empty_like(out)]
+        works = [qd.gather_logits_async(model_fn(x[s:e]), bufs[k]) for k in range(2)]
+        for wk in works:
+            wk.wait()
+        for bf in bufs:
+            assert torch.equal(bf, out)
         q.put((rank, out.numpy()))
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
