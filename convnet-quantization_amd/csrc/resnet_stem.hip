@@ -32,15 +32,23 @@
 
 namespace qcn {
 
-// per-byte max of four u8 lanes (two packed u16 maxes)
-QCN_DEV uint32_t stem_max_u8x4(uint32_t a, uint32_t b) {
-  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-  const uint32_t m = 0x00ff00ffu;
-  const us2 a0 = __builtin_bit_cast(us2, a & m), b0 = __builtin_bit_cast(us2, b & m);
-  const us2 a1 = __builtin_bit_cast(us2, (a >> 8) & m), b1 = __builtin_bit_cast(us2, (b >> 8) & m);
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(a0, b0)) |
-         (__builtin_bit_cast(uint32_t, __builtin_elementwise_max(a1, b1)) << 8);
-}
+// Per-byte max of u8 x 4 dwords, kept split as two packed u16 pairs: the
+// even bytes (0, 2) and the odd bytes (1, 3) of each dword, zero-extended.
+// Per tap dword: one AND, one v_perm, two v_pk_max_u16; joined once at the end.
+typedef unsigned short stem_us2 __attribute__((ext_vector_type(2)));
+struct StemMax {
+  stem_us2 lo, hi;
+  QCN_DEV void add(uint32_t s) {
+    const stem_us2 sl = __builtin_bit_cast(stem_us2, s & 0x00ff00ffu);
+    // bytes 1 and 3 of s into bytes 0 and 2, zeros (selector 0x0c) above them
+    const stem_us2 sh = __builtin_bit_cast(stem_us2, __builtin_amdgcn_perm(0u, s, 0x0c030c01u));
+    lo = __builtin_elementwise_max(lo, sl);
+    hi = __builtin_elementwise_max(hi, sh);
+  }
+  QCN_DEV uint32_t get() const {
+    return __builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8);
+  }
+};
 
 template <int S>
 struct StemCfg {
@@ -241,7 +249,9 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
     // ---- D: 3x3/2 max-pool (pool row pr0 + pr reads local conv rows 2 pr .. 2 pr + 2)
     for (int e = tid; e < C::P * C::PW * 4; e += C::NTH) {
       const int q16 = e & 3, pc = (e >> 2) % C::PW, pr = (e >> 2) / C::PW;
-      uint32_t r[4] = {0u, 0u, 0u, 0u};
+      StemMax r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k].lo = r[k].hi = (stem_us2){0, 0};
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy) {
         const int lr = 2 * pr + dy;
@@ -252,11 +262,11 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
           if (cx < 0) continue;
           const uint32_t* s = reinterpret_cast<const uint32_t*>(r2 + (lr * C::OW + cx) * C::CSP + 16 * q16);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) r[k] = stem_max_u8x4(r[k], s[k]);
+          for (int k = 0; k < 4; ++k) r[k].add(s[k]);
         }
       }
       uint8_t* o = a.y + ((((long)img * C::PW + pr0 + pr) * C::PW + pc) * C::C + 16 * q16);
-      *reinterpret_cast<uint4*>(o) = make_uint4(r[0], r[1], r[2], r[3]);
+      *reinterpret_cast<uint4*>(o) = make_uint4(r[0].get(), r[1].get(), r[2].get(), r[3].get());
     }
     __syncthreads();   // QIN (next phase A) aliases CS
   }
