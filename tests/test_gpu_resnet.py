@@ -71,6 +71,10 @@ def test_conv_general_golden(dev, golden_dir, impl):
     (1, 1, 1, 64, 128, 3, 3, 1, 1, 13, True, 0, True),
     (2, 56, 56, 64, 64, 3, 3, 1, 1, 0, True, 0, True),
     (1, 28, 28, 128, 512, 1, 1, 1, 0, 9, False, 140, True),
+    # 256-channel 8-wave tiles (3x3 and 2048-deep 1x1, cout % 256 == 0), ragged pixel counts
+    (3, 9, 11, 128, 256, 3, 3, 1, 1, 31, True, 0, True),
+    (2, 13, 13, 64, 512, 3, 3, 2, 1, 200, False, 77, False),
+    (2, 5, 7, 2048, 512, 1, 1, 1, 0, 3, True, 0, True),
 ])
 @pytest.mark.parametrize("impl", ["gemm", "gen"])
 def test_conv_general_oracle(dev, shape, impl):
