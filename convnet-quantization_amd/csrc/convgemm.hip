@@ -135,6 +135,9 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   // npix < 2^31 is checked at launch), each lane's offset (< 256) is carried
   // through ox and oy with small fp32-reciprocal divisions — no 64-bit
   // divisions per lane (they were ~half the VALU of the thin 1x1 convs)
+  // A 1x1 stride-1 unpadded conv reads input pixel = output pixel: no
+  // decomposition and no bounds checks (uniform branch).
+  const bool flat = a.kh == 1 && a.kw == 1 && a.sy == 1 && a.sx == 1 && a.py == 0 && a.px == 0;
   const int ohw = a.oh * a.ow;
   const int m0i = (int)m0;
   const int img0 = m0i / ohw, rem0 = m0i - img0 * ohw;
@@ -144,6 +147,11 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   for (int e = 0; e < C::NB; ++e) {
     const int off = (wave + C::NW * e) * 16 + (lane >> 2);
     pv[e] = m0 + off < a.npix;
+    if (flat) {
+      iy0[e] = ix0[e] = 0;
+      pbase[e] = (m0 + off) * (long)a.cin + bh * 16;
+      continue;
+    }
     const int tx = ox00 + off;
     const int qx = div_small(tx, a.ow, rw);
     const int ty = oy00 + qx;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
 #pragma unroll
     for (int e = 0; e < C::NB; ++e) {      // B: instruction wave + NW e
       const int iy = iy0[e] + lr, ix = ix0[e] + ls;
-      const bool in = live && pv[e] && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w_;
+      const bool in = live && pv[e] && (flat || (iy >= 0 && iy < a.h && ix >= 0 && ix < a.w_));
       const void* src = in ? (const void*)(a.x + pbase[e] + toff) : (const void*)zpl;
       glds16(src, buf + C::AREG + (wave + C::NW * e) * 1024);
     }
