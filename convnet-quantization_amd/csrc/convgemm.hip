@@ -207,31 +207,25 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
 #pragma unroll
     for (int j = 0; j < C::JT; ++j) acc[i][j] = c0;
   }
-  // Residual join (RESID): the identity bytes each thread's phase-2 rows need
-  // (constant row set per thread, see the epilogue).  With at most two stages
-  // (conv3 with K <= 128) they are loaded right behind the stage DMAs, so
-  // their HBM latency overlaps the DMA wait and the MFMAs instead of following
-  // them; longer K loads them before the requant phase.  Rows past npix load
-  // the last pixel's bytes (unused) so every wave issues the same count.
-  // The join runs in passes p = (channel half i, wave-column pair h): the
-  // waves of columns 2h, 2h + 1 stage their 32-channel half i, R_NCOL columns.
-  constexpr int NSUB = C::WN > 2 ? C::WN / 2 : 1, NPASS = 2 * NSUB;
-  constexpr int R_NCOL = 32 * (C::WN < 2 ? C::WN : 2);   // staged columns per pass
-  constexpr int R_TPR = R_NCOL / 16, R_RPI = C::NT / R_TPR, NIT = C::BM / R_RPI;
-  constexpr int NIDL = NPASS * NIT;            // identity loads per thread
-  const int rr = tid / R_TPR, cq = tid % R_TPR;   // phase-2 row / 16-column group
-  const int ch2 = n0 + 64 * ((cq * 16) / 32) + (cq * 16) % 32;   // + 32 i + 128 h
-  uint4 rid[NPASS][NIT];
+  // Residual join (RESID): the identity bytes each thread's join rows need
+  // (thread (rr, cq): 16 channels of rows rr + R_RPI it, see the epilogue).
+  // With at most two stages (conv3 with K <= 128) they are loaded right
+  // behind the stage DMAs, so their HBM latency overlaps the DMA wait and the
+  // MFMAs instead of following them; longer K loads them before the join.
+  // Rows past npix load the last pixel's bytes (unused) so every wave issues
+  // the same count.
+  constexpr int R_TPR = BN / 16, R_RPI = C::NT / R_TPR, NIT = C::BM / R_RPI;
+  constexpr int NIDL = NIT;                    // identity loads per thread
+  const int rr = tid / R_TPR, cq = tid % R_TPR;
+  const int ch2 = n0 + cq * 16;
+  uint4 rid[NIT];
   auto load_id = [&]() {
 #pragma unroll
-    for (int p = 0; p < NPASS; ++p)
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        long pp = m0 + it * R_RPI + rr;
-        pp = pp < a.npix ? pp : a.npix - 1;
-        rid[p][it] = *reinterpret_cast<const uint4*>(a.r + pp * a.cout + ch2 + 32 * (p / NSUB) +
-                                                     128 * (p % NSUB));
-      }
+    for (int it = 0; it < NIT; ++it) {
+      long pp = m0 + it * R_RPI + rr;
+      pp = pp < a.npix ? pp : a.npix - 1;
+      rid[it] = *reinterpret_cast<const uint4*>(a.r + pp * a.cout + ch2);
+    }
   };
   const bool early = RESID && nst <= 2;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -311,99 +305,6 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   __builtin_amdgcn_s_barrier();   // every wave is done with the ring: reuse it
   __builtin_amdgcn_sched_barrier(0);
 
-  if constexpr (RESID) {
-    // Residual join: per channel half i, phase 1 writes the dequantized conv
-    // output d3 = s3*(y3 - z3) as fp32 — y3 - z3 = med3(rint(ab), -z3, 255-z3)
-    // exactly (conv3 has no ReLU), so the u8 y3 is never materialised — into
-    // an LDS tile [BM][32*WN floats]; phase 2 reads it row-contiguous next to
-    // the coalesced identity bytes: out = quantize(relu(d3 + s_r*(r - z_r))).
-    constexpr int OSF = R_NCOL * 4 + 16;       // fp32 row stride (bytes)
-    constexpr int RPI = R_RPI;
-    static_assert(C::BM * OSF <= C::LDS, "fp32 staging fits in the ring");
-    const v2f nz3 = {-(float)a.zp_y, -(float)a.zp_y}, hz3 = {255.0f - a.zp_y, 255.0f - a.zp_y};
-    const v2f s3 = {a.s3, a.s3};
-    // longer K: the identity bytes of both halves' phase 2, loaded before
-    // phase 1 so their HBM latency hides behind the requant math
-    if (!early) load_id();
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int i = p / NSUB, hsub = p % NSUB;
-      const int co0 = n0 + wc * 64 + i * 32;
-      v2f u[8], v[8], mu[8];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co = co0 + 8 * g + 4 * hi;
-        const float4 x4 = *reinterpret_cast<const float4*>(a.u + co);
-        const float4 y4 = *reinterpret_cast<const float4*>(a.v + co);
-        const float4 z4 = *reinterpret_cast<const float4*>(a.mult + co);
-        u[2 * g] = (v2f){x4.x, x4.y}; u[2 * g + 1] = (v2f){x4.z, x4.w};
-        v[2 * g] = (v2f){y4.x, y4.y}; v[2 * g + 1] = (v2f){y4.z, y4.w};
-        mu[2 * g] = (v2f){z4.x, z4.y}; mu[2 * g + 1] = (v2f){z4.z, z4.w};
-      }
-#pragma unroll
-      for (int j = 0; j < C::JT; ++j) {
-        if (NSUB > 1 && (wc >> 1) != hsub) break;   // another pass's columns
-        uint8_t* rowp = lds + ((wm * C::JT + j) * 32 + l32) * OSF + ((wc & 1) * 32) * 4;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          v2f d[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int h2 = 2 * g + h;
-            const v2f ab = requant2(acc[i][j][2 * h2], acc[i][j][2 * h2 + 1], u[h2], v[h2], mu[h2]);
-            d[h] = (v2f){__builtin_amdgcn_fmed3f(__builtin_rintf(ab.x), nz3.x, hz3.x),
-                         __builtin_amdgcn_fmed3f(__builtin_rintf(ab.y), nz3.x, hz3.x)} * s3;
-          }
-          *reinterpret_cast<float4*>(rowp + (8 * g + 4 * hi) * 4) = make_float4(d[0].x, d[0].y, d[1].x, d[1].y);
-        }
-      }
-      __syncthreads();
-      const v2f zr = {(float)a.z_r, (float)a.z_r}, sr = {a.s_r, a.s_r}, io = {a.inv_o, a.inv_o};
-      const float zof = (float)a.z_o;
-      auto join = [&](auto zo0) {
-        constexpr bool ZO0 = decltype(zo0)::value;   // z_o == 0: ReLU = saturation at 0
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-          const int row = it * RPI + rr;
-          const long px = m0 + row;
-          if (px >= a.npix) break;
-          const long off = px * a.cout + ch2 + 32 * i + 128 * hsub;
-          const uint4 rv = rid[p][it];
-          const float4* dp = reinterpret_cast<const float4*>(lds + row * OSF + cq * 64);
-          const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
-          uint32_t ow[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 d4 = dp[g];
-            uint32_t o = 0;
-#pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const v2f rf = {(float)((rw[g] >> (8 * e)) & 0xff), (float)((rw[g] >> (8 * e + 8)) & 0xff)};
-              const v2f dd = e ? (v2f){d4.z, d4.w} : (v2f){d4.x, d4.y};
-              const v2f sm = (dd + (rf - zr) * sr) * io;
-              if constexpr (ZO0) {
-                o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
-                o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
-              } else {   // relu(s) * inv == max(s * inv, 0) since inv > 0
-                o = __builtin_amdgcn_cvt_pk_u8_f32(
-                    __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f),
-                    e, o);
-                o = __builtin_amdgcn_cvt_pk_u8_f32(
-                    __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f),
-                    e + 1, o);
-              }
-            }
-            ow[g] = o;
-          }
-          *reinterpret_cast<uint4*>(a.y + off) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-        }
-      };
-      if (a.z_o == 0) join(std::true_type{});
-      else join(std::false_type{});
-      __syncthreads();
-    }
-    return;
-  }
 
   // Epilogue phase 1 (accumulator layout: lane (l32, hi) of tile (i, j) holds
   // pixel l32, channels 8g + 4hi + e): FBGEMM requant to u8 — scalar fma / mul
@@ -471,6 +372,57 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
     }
   }
   __syncthreads();
+
+  if constexpr (RESID) {
+    // Residual join on the staged u8 conv3 output y3 (phase 1 above, zp z3, no
+    // ReLU): out = quantize(relu(s3*(y3 - z3) + s_r*(r - z_r))) with the
+    // identity r loaded earlier (rid) — (float)y3 - z3 is exact, so this is
+    // the same fp32 op sequence as qcn_add_relu_u8 on the materialised y3.
+    // Row-contiguous: thread (rr, cq) takes 16 channels of rows rr + R_RPI it.
+    if (!early) load_id();
+    const v2f z3v = {(float)a.zp_y, (float)a.zp_y}, s3v = {a.s3, a.s3};
+    const v2f zr = {(float)a.z_r, (float)a.z_r}, sr = {a.s_r, a.s_r}, io = {a.inv_o, a.inv_o};
+    const float zof = (float)a.z_o;
+    auto join = [&](auto zo0) {
+      constexpr bool ZO0 = decltype(zo0)::value;   // z_o == 0: ReLU = saturation at 0
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = it * R_RPI + rr;
+        const long px = m0 + row;
+        if (px >= a.npix) break;
+        const uint4 yv = *reinterpret_cast<const uint4*>(lds + row * C::OS + cq * 16);
+        const uint4 rv = rid[it];
+        const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w}, rw[4] = {rv.x, rv.y, rv.z, rv.w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const v2f yf = {(float)((yw[g] >> (8 * e)) & 0xff), (float)((yw[g] >> (8 * e + 8)) & 0xff)};
+            const v2f rf = {(float)((rw[g] >> (8 * e)) & 0xff), (float)((rw[g] >> (8 * e + 8)) & 0xff)};
+            const v2f sm = ((yf - z3v) * s3v + (rf - zr) * sr) * io;
+            if constexpr (ZO0) {
+              o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
+              o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
+            } else {   // relu(s) * inv == max(s * inv, 0) since inv > 0
+              o = __builtin_amdgcn_cvt_pk_u8_f32(
+                  __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f),
+                  e, o);
+              o = __builtin_amdgcn_cvt_pk_u8_f32(
+                  __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f),
+                  e + 1, o);
+            }
+          }
+          ow[g] = o;
+        }
+        *reinterpret_cast<uint4*>(a.y + px * a.cout + ch2) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      }
+    };
+    if (a.z_o == 0) join(std::true_type{});
+    else join(std::false_type{});
+    return;
+  }
 
   // Epilogue phase 2 (row-contiguous): 16 B per thread, whole 64/128-B row
   // segments per store instruction.
