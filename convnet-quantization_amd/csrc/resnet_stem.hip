@@ -116,6 +116,11 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
       wa[i][r] = *reinterpret_cast<const v4i*>(a.w + ((r * 64) + 32 * i + l32) * 32 + 16 * hi);
 
   const int nb = a.n * C::BANDS;
+  // a contiguous run of bands per workgroup (mostly one image, top to
+  // bottom): the 7 input rows two neighbouring bands share were fetched by
+  // this CU one band earlier and come from its XCD's L2, not HBM
+  const int bbeg = (int)((long)blockIdx.x * nb / gridDim.x);
+  const int bend = (int)((long)(blockIdx.x + 1) * nb / gridDim.x);
   // phase-A prefetch: item it = tid + NTH k -> (QIN row, 4-column group)
   float4 pf[C::NPF][3];
   auto prefetch = [&](int band) {
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
       const int it = tid + C::NTH * k;
       const int row = it / (S / 4), c4 = it % (S / 4);
       const int iy = 4 * pr0 - 5 + row;
-      const bool ok = band < nb && it < C::ITEMS && iy >= 0 && iy < S;
+      const bool ok = band < bend && it < C::ITEMS && iy >= 0 && iy < S;
 #pragma unroll
       for (int c = 0; c < 3; ++c)
         pf[k][c] = ok ? *reinterpret_cast<const float4*>(a.x + (((long)img * 3 + c) * S + iy) * S + 4 * c4)
@@ -138,9 +143,9 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
     return (uint32_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
   };
 
-  int band = blockIdx.x;
+  int band = bbeg;
   prefetch(band);
-  for (; band < nb; band += gridDim.x) {
+  for (; band < bend; ++band) {
     const int img = band / C::BANDS, pr0 = (band % C::BANDS) * C::P;
     // ---- A: quantize the input rows into QIN (3 B per column, channel fastest)
 #pragma unroll
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
     }
     __syncthreads();
     // next band's input: in flight during C and D
-    prefetch(band + gridDim.x);
+    prefetch(band + 1);
     // ---- C: conv tiles -> requant + ReLU -> CS [conv px][CSP]
     const bool row0_pad = pr0 == 0;   // local conv row 0 is conv row -1 (pool padding)
     for (int t = wave; t < C::NT; t += C::NTH / 64) {

@@ -14,7 +14,7 @@ def rows(tag):
         return []
     per = {}
     for r in csv.DictReader(open(f[0])):
-        if "conv_gemm_kernel" not in r["Kernel_Name"]:
+        if "conv_gemm_kernel" not in r["Kernel_Name"] and "stem_fused_kernel" not in r["Kernel_Name"]:
             continue
         d = per.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -23,7 +23,7 @@ def rows(tag):
 
 
 sq, fe, wr = rows("sq"), rows("fetch"), rows("write")
-n = 53   # conv launches per forward
+n = 53   # conv launches per forward (the fused stem counts as the first)
 sq, fe, wr = sq[-n:], fe[-n:], wr[-n:]
 print("idx  valuM  mfmaM  ldsM  waitany  waitinst  mfma_busy  fetchMB  writeMB")
 for i in range(min(len(sq), len(fe), len(wr))):
