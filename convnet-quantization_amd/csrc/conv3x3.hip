@@ -27,26 +27,11 @@
 #include <type_traits>
 #include <cstdlib>
 
-// Diagnostic build only (tools/micro/conv_stamp.hip defines QCN_STAMPS):
-// wave 0 of each workgroup records s_memtime at phase boundaries.
-#ifdef QCN_STAMPS
-__device__ unsigned long long qcn_stamps[1 << 16][8];
-#define QCN_STAMP(k)                                                              \
-  do {                                                                            \
-    if (threadIdx.x == 0) {                                                       \
-      qcn_stamps[blockIdx.x & 0xffff][k] = __builtin_amdgcn_s_memtime();          \
-      if (k == 0 || k == 5) qcn_stamps[blockIdx.x & 0xffff][6 + k / 5] = __builtin_amdgcn_s_memrealtime(); \
-    }                                                                             \
-  } while (0)
-#else
-#define QCN_STAMP(k) do {} while (0)
-#endif
-
-#ifndef QCN_PROD_PRIO
-#define QCN_PROD_PRIO 2   // conv12 producer waves' issue priority
-#endif
-
 namespace qcn {
+
+// conv12 producer waves' issue priority (swept: 1-3 within noise, 2 best;
+// 0 is ~20 % slower, profiles/r01_diag_conv12_prio_sweep_v16.txt)
+constexpr int kProdPrio = 2;
 
 // Patch layout knobs (chosen per layer by an offline bank-conflict search so
 // that every ds_read_b128 of an MFMA operand is conflict-free):
@@ -575,7 +560,6 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int lane = tid & 63;
   const int wave = tid >> 6;
 
-  QCN_STAMP(0);
   const long p0 = (long)blockIdx.x * C::PXB;         // first output pixel (pre-pool)
   const int n0 = (int)(p0 / C::IMG);
   const int y0 = (int)((p0 % C::IMG) / C::W);
@@ -583,13 +567,9 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   stage_epik<COUT, C::NT>(ep, reinterpret_cast<float*>(lds + C::EPI), tid);
   stage_patch<C>(x, nimg, x_zp, n0, y0, patch, tid);
 
-  QCN_STAMP(1);
-  QCN_STAMP(2);
   v16i acc[C::WI][4];
   conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
-  QCN_STAMP(3);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y, (int)blockIdx.x);
-  QCN_STAMP(5);
 }
 
 // --------------------------------------------------------------------------
@@ -631,15 +611,12 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
   const int y0 = (int)((p0 % CA::IMG) / CA::W);
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
-  QCN_STAMP(0);
   stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
   stage_patch<CA, BYPASS_L1>(x, nimg, x_zp, n0, y0, lds, tid);
-  QCN_STAMP(1);
 
   v16i acc[CA::WI][4];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
-  QCN_STAMP(2);
 
   // ---- A's epilogue into B's patch (A's patch and ring are dead past the
   // main loop's final barrier): zero-point halo, then the requantized interior
@@ -673,11 +650,8 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
     }
   }
   __syncthreads();
-  QCN_STAMP(3);
   conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
-  QCN_STAMP(4);
   conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
-  QCN_STAMP(5);
 }
 
 template <class CA, class CB>
@@ -685,12 +659,6 @@ __global__ __launch_bounds__(CA::NT, CA::WI == 4 ? 1 : 2)
 void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                      const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                      const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
-#ifdef QCN_STAMPS   // where each workgroup ran: HW_ID (CU, SE, slot) and XCC_ID
-  if (threadIdx.x == 0) {
-    qcn_stamps[(blockIdx.x + 16384) & 0xffff][0] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));
-    qcn_stamps[(blockIdx.x + 16384) & 0xffff][1] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));
-  }
-#endif
   convpair_body<CA, CB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
@@ -1051,7 +1019,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
                         int step) {
     // producer waves issue first: their VALU-bound conv1 is the longer phase,
     // the consumer's MFMAs fill the gaps (measured 53.6 vs 59.2 us)
-    __builtin_amdgcn_s_setprio(QCN_PROD_PRIO);
+    __builtin_amdgcn_s_setprio(kProdPrio);
     const int h = t & 1, y0 = h * 16;
     const int r0 = h == 0 ? 1 : (prev ? 2 : 0), r1 = h == 0 ? 18 : 17;
     const int ln = fresh(lane), l32 = ln & 31, hi = ln >> 5;
@@ -1229,10 +1197,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
                                               dst, wbase, woff);
   };
 
-#ifdef QCN_STAMPS
-  unsigned long long busy = 0, bwait = 0, pa_ = 0, pb_ = 0, t_start = __builtin_amdgcn_s_memtime();
-  if (tid == 0) qcn_stamps[blockIdx.x & 0xffff][6] = __builtin_amdgcn_s_memrealtime();
-#endif
   if (producer && T > 0) stage_load(tile_of(0));
   setup();
   if (producer && T > 0) stage_store(in8_0, 0);
@@ -1246,30 +1210,16 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     vuni = __builtin_amdgcn_ballot_w64(ek1[64 + l] != ek1[64]) == 0;
     muni = __builtin_amdgcn_ballot_w64(ek1[128 + l] != ek1[128]) == 0;
   }
-#ifdef QCN_STAMPS
-  const unsigned long long t_pro = __builtin_amdgcn_s_memtime();
-#endif
   constexpr bool SPLIT0 = true;
   for (int j = 0; j <= T; ++j) {
-#ifdef QCN_STAMPS
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
     if (producer) {
       if (j + 1 < T) stage_load(tile_of(j + 1));
-#ifdef QCN_STAMPS
-      const unsigned long long ta_ = __builtin_amdgcn_s_memtime();
-      pa_ += ta_ - t0;
-#endif
       if (j < T) {
         // the first tile's conv1 is split with the (otherwise idle) consumer waves
         const bool split = SPLIT0 && j == 0;
         conv1_tile(tile_of(j), (j & 1) ? in8_1 : in8_0, (j & 1) ? patch1 : patch0,
                    (j & 1) ? patch0 : nullptr, split ? wave : wave - 4, split ? 8 : 4);
       }
-#ifdef QCN_STAMPS
-      const unsigned long long tb_ = __builtin_amdgcn_s_memtime();
-      pb_ += tb_ - ta_;
-#endif
       if (j + 1 < T) stage_store(((j + 1) & 1) ? in8_1 : in8_0, (j + 1) & 1);
     } else if (j >= 1) {
       conv2_tile(tile_of(j - 1), ((j - 1) & 1) ? patch1 : patch0);
@@ -1277,43 +1227,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       conv1_tile(tile_of(0), in8_0, patch0, nullptr, wave, 8);
       __builtin_amdgcn_s_setprio(0);
     }
-#ifdef QCN_STAMPS
-    const unsigned long long tw = __builtin_amdgcn_s_memtime();
-    busy += tw - t0;
-#endif
     __syncthreads();
-#ifdef QCN_STAMPS
-    bwait += __builtin_amdgcn_s_memtime() - tw;
-#endif
   }
-#ifdef QCN_STAMPS
-  // per role: barrier wait, and the loop's elapsed time (waves 0 and 4)
-  if (tid == 0 || tid == 256) {
-    qcn_stamps[(blockIdx.x + 8192) & 0xffff][tid ? 1 : 0] = bwait;
-    qcn_stamps[(blockIdx.x + 8192) & 0xffff][tid ? 3 : 2] = __builtin_amdgcn_s_memtime() - t_pro;
-  }
-#endif
-#ifdef QCN_STAMPS
-  // [0] start, [1] +prologue, [2] +consumer busy (wave 0), [3] +producer busy (wave 4), [5] end
-  if (tid == 0) {
-    qcn_stamps[blockIdx.x & 0xffff][0] = t_start;
-    qcn_stamps[blockIdx.x & 0xffff][1] = t_pro;
-    qcn_stamps[blockIdx.x & 0xffff][2] = t_pro + busy;
-  }
-  __syncthreads();
-  if (tid == 256) {
-    qcn_stamps[blockIdx.x & 0xffff][3] = qcn_stamps[blockIdx.x & 0xffff][2] + busy;
-    qcn_stamps[(blockIdx.x + 4096) & 0xffff][0] = pa_;   // producer: stage_load issue
-    qcn_stamps[(blockIdx.x + 4096) & 0xffff][1] = pb_;   // producer: conv1
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned long long e = __builtin_amdgcn_s_memtime();
-    qcn_stamps[blockIdx.x & 0xffff][4] = qcn_stamps[blockIdx.x & 0xffff][3];
-    qcn_stamps[blockIdx.x & 0xffff][5] = e > qcn_stamps[blockIdx.x & 0xffff][4] ? e : qcn_stamps[blockIdx.x & 0xffff][4];
-    qcn_stamps[blockIdx.x & 0xffff][7] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
 }
 
 __global__ __launch_bounds__(512, 1)
