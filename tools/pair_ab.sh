@@ -1,5 +1,5 @@
 # Same-box A/B of env variants on the full forward (kbench) with per-kernel times.
-# usage (on the box): bash tools/pair_ab.sh "QCN_PAIR_WI=2" "QCN_PAIR_WI=4" ...
+# usage (on the box): bash tools/pair_ab.sh "QCN_FC_HEAD=fused" "QCN_FC_HEAD=linear" ...
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pab
