@@ -28,11 +28,15 @@ constexpr int FC_N2 = 16;    // max fc2 outputs
 
 // X' [K/32][m][32], W' [K/32][n][32] (chunk-major: a 32-row MFMA fragment of
 // one 32-byte K chunk is one contiguous 1 KB, every wave-load fully coalesced).
+// RW: rows per wave — 64 (two MFMA row blocks, 128-row workgroups) or 32
+// (one block, 64-row workgroups: twice the workgroups at the same partial
+// traffic, for batches too small to fill the CUs with 128-row tiles).
+template <int RW>
 __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restrict__ x, int m, int k,
                                                         const int8_t* __restrict__ w, int n,
                                                         int* __restrict__ part) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int MB = m / 128, NB = n / 64, T = MB * NB * FC_S;
+  const int MB = m / (2 * RW), NB = n / 64, T = MB * NB * FC_S;
   int mb, nb, s;
   if (T % 8 == 0 && (MB * NB) % 2 == 0) {
     // K-quarter-major over the XCDs (workgroup b runs on XCD b % 8): XCD x
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
     s = rem % FC_S;
   }
   const int mi = wave & 1, ni = wave >> 1;
-  const int row0 = mb * 128 + mi * 64, col0 = nb * 64 + ni * 32;
+  const int row0 = mb * 2 * RW + mi * RW, col0 = nb * 64 + ni * 32;
   const int kcs = (k / 32) / FC_S, kc0 = s * kcs;
   // fragment lane (l32, hi): row l32, bytes [16 hi, 16 hi + 16) of the chunk
   const int frag = (lane & 31) * 32 + (lane >> 5) * 16;
@@ -71,17 +75,20 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
     for (int u = 0; u < U; ++u) {
       fw[buf][u] = *reinterpret_cast<const v4i*>(wa + (c + u) * ws);
       f0[buf][u] = *reinterpret_cast<const uint4*>(xa + (c + u) * xs);
-      f1[buf][u] = *reinterpret_cast<const uint4*>(xa + (c + u) * xs + 1024);
+      if constexpr (RW == 64) f1[buf][u] = *reinterpret_cast<const uint4*>(xa + (c + u) * xs + 1024);
     }
   };
   auto mm = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint4 a = f0[buf][u], b = f1[buf][u];
+      const uint4 a = f0[buf][u];
       const v4i b0 = (v4i){(int)xor80(a.x), (int)xor80(a.y), (int)xor80(a.z), (int)xor80(a.w)};
-      const v4i b1 = (v4i){(int)xor80(b.x), (int)xor80(b.y), (int)xor80(b.z), (int)xor80(b.w)};
       acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b1, acc1, 0, 0, 0);
+      if constexpr (RW == 64) {
+        const uint4 b = f1[buf][u];
+        const v4i b1 = (v4i){(int)xor80(b.x), (int)xor80(b.y), (int)xor80(b.z), (int)xor80(b.w)};
+        acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(fw[buf][u], b1, acc1, 0, 0, 0);
+      }
     }
   };
   load(0, 0);
@@ -101,8 +108,21 @@ __global__ __launch_bounds__(256) void fc_splitk_kernel(const uint8_t* __restric
   for (int g = 0; g < 4; ++g) {
     *reinterpret_cast<int4*>(pp + (long)r * n + 8 * g) =
         make_int4(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
-    *reinterpret_cast<int4*>(pp + (long)(r + 32) * n + 8 * g) =
-        make_int4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+    if constexpr (RW == 64)
+      *reinterpret_cast<int4*>(pp + (long)(r + 32) * n + 8 * g) =
+          make_int4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+  }
+}
+
+// 64-row tiles below 1024 rows (batch 256: 128 workgroups instead of 64)
+inline void launch_fc_splitk(const uint8_t* x, int m, int k, const int8_t* w1, int n1, int* part,
+                             hipStream_t st) {
+  if (m < 1024) {
+    const int tiles = (m / 64) * (n1 / 64) * FC_S;
+    hipLaunchKernelGGL(fc_splitk_kernel<32>, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
+  } else {
+    const int tiles = (m / 128) * (n1 / 64) * FC_S;
+    hipLaunchKernelGGL(fc_splitk_kernel<64>, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
   }
 }
 
@@ -332,8 +352,7 @@ int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1
     return QCN_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   int* part = static_cast<int*>(workspace);
-  const int tiles = (m / 128) * (n1 / 64) * qcn::FC_S;
-  hipLaunchKernelGGL(qcn::fc_splitk_kernel, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
+  qcn::launch_fc_splitk(x, m, k, w1, n1, part, st);
   qcn::FcHead hd{u1, v1, mult1, corr1, y1_zp, relu1 ? y1_zp : 0, w2, n2, u2, v2, mult2,
                  y2_zp, relu2 ? y2_zp : 0, y2_scale};
   hipLaunchKernelGGL(qcn::fc_finish_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd, y1,
@@ -353,8 +372,7 @@ int qcn_classifier_qdq_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, in
     return QCN_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   int* part = static_cast<int*>(workspace);
-  const int tiles = (m / 128) * (n1 / 64) * qcn::FC_S;
-  hipLaunchKernelGGL(qcn::fc_splitk_kernel, dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, part);
+  qcn::launch_fc_splitk(x, m, k, w1, n1, part, st);
   qcn::FcHeadQdq hd{u1, v1, mult1, corr1, y1_zp, 0, y1_scale, w2, b2, n2};
   hipLaunchKernelGGL(qcn::fc_finish_qdq_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd,
                      y1, y2);
