@@ -25,7 +25,6 @@ import csv
 import glob
 import json
 import os
-import pickle
 import shutil
 import signal
 import subprocess
@@ -73,8 +72,61 @@ HBM_BOUND = {"conv1"}
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
                   "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256",),
-                  "fc12": ("fc_splitk_kernel", "fc_finish_kernel"),
+                  # "fc_finish" matches fc_finish_kernel (static) and fc_finish_qdq_kernel (QDQ)
+                  "fc12": ("fc_splitk_kernel", "fc_finish"),
                   "fc1": ("linear_u8s8_kernel",), "fc2": ("linear_f32_kernel",)}
+
+
+# The parent hands its model to the counter-pass children through a file in a
+# no-code format: torch.save of tensors / dicts / lists / primitives only, read
+# back with torch.load(weights_only=True).  numpy arrays and scalars are tagged
+# so they come back with their exact dtype.
+def _enc(o):
+    if isinstance(o, np.ndarray):
+        return {"__nd__": torch.from_numpy(np.ascontiguousarray(o))}
+    if isinstance(o, np.generic):
+        return {"__np__": str(o.dtype), "v": o.item()}
+    if isinstance(o, dict):
+        return {"__dict__": [[_enc(k), _enc(v)] for k, v in o.items()]}
+    if isinstance(o, (list, tuple)):
+        return {"__seq__": type(o).__name__, "v": [_enc(x) for x in o]}
+    if isinstance(o, torch.Tensor):
+        return {"__t__": o.detach().cpu()}
+    if o is None or isinstance(o, (bool, int, float, str)):
+        return o
+    raise TypeError(f"payload: cannot encode {type(o).__name__}")
+
+
+def _dec(o):
+    if isinstance(o, dict):
+        if "__nd__" in o:
+            return o["__nd__"].numpy()
+        if "__np__" in o:
+            return np.dtype(o["__np__"]).type(o["v"])
+        if "__dict__" in o:
+            return {_dec(k): _dec(v) for k, v in o["__dict__"]}
+        if "__seq__" in o:
+            v = [_dec(x) for x in o["v"]]
+            return tuple(v) if o["__seq__"] == "tuple" else v
+        if "__t__" in o:
+            return o["__t__"]
+    return o
+
+
+def save_payload(path, payload):
+    torch.save(_enc(payload), path)
+
+
+def load_payload(path):
+    return _dec(torch.load(path, weights_only=True))
+
+
+def under_profiler():
+    """True when this process already runs under rocprofv3 (its preloaded tool
+    library initialised the GPU before main): a nested rocprofv3 child would then
+    be an exec from a GPU-initialised process tree, which the box refuses."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    return ("rocprof" in pre or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ))
 
 
 def build_model(rank, device, per_channel=False, spec_file=None, mode="static"):
@@ -84,8 +136,7 @@ def build_model(rank, device, per_channel=False, spec_file=None, mode="static"):
     from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state_dict
     payload = None
     if spec_file:   # a counter pass: the parent's model, written by this script
-        with open(spec_file, "rb") as f:
-            payload = pickle.load(f)
+        payload = load_payload(spec_file)
     elif rank == 0:
         # trained on the synthetic 10-class task (no CIFAR-10 / checkpoint offline)
         x_cal, _ = data.synthetic_task(512, 1)
@@ -235,11 +286,13 @@ def cpu_baseline_qdq(state_dict, qmodel_gpu, seconds):
 # collected the way MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes:
 # one pass per counter group, FETCH_SIZE doubled on gfx950 (it tallies 128-B
 # requests at 64 B), WRITE_SIZE as is, both in KiB per dispatch; the clock as
-# GRBM_GUI_ACTIVE / 8 XCDs / kernel time on a batch-8192 dispatch (long enough
-# for the quotient to be accurate).
+# mfma_busy as SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of
+# the same batch-B dispatch.  GRBM_GUI_ACTIVE / 8 / wall time reads high on
+# dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md 'DVFS give-back'), so the
+# clock the chip holds is measured in-kernel instead (tools/clock: s_memtime /
+# s_memrealtime around each workgroup of a diagnostic build, see clock_pass()).
 PMC_PASSES = (("fetch", ("FETCH_SIZE",), None),
-              ("write", ("WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"), None),
-              ("clock", ("GRBM_GUI_ACTIVE",), 8192))
+              ("write", ("WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"), None))
 
 
 def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static"):
@@ -298,9 +351,9 @@ def _per_launch(agg, launch, counter):
 
 def pmc_counters(model, sd, args, names, timeout=150):
     """Counter passes for every launch; returns ({launch: {...}}, error text)."""
-    fd, spec_file = tempfile.mkstemp(prefix="qcn_spec_", suffix=".pkl", dir="/tmp")
-    with os.fdopen(fd, "wb") as f:
-        pickle.dump((model.spec, sd), f)
+    fd, spec_file = tempfile.mkstemp(prefix="qcn_spec_", suffix=".pt", dir="/tmp")
+    os.close(fd)
+    save_payload(spec_file, (model.spec, sd))
     res = {n: {} for n in names}
     errors = []
     try:
@@ -315,6 +368,8 @@ def pmc_counters(model, sd, args, names, timeout=150):
                 if tag == "fetch":
                     v = _per_launch(agg, n, "FETCH_SIZE")
                     res[n]["fetch_bytes"] = None if v is None else 2.0 * v * 1024
+                    if v is None:
+                        errors.append(f"{tag}: no counter row matched launch {n}")
                 elif tag == "write":
                     v = _per_launch(agg, n, "WRITE_SIZE")
                     res[n]["write_bytes"] = None if v is None else v * 1024
@@ -325,12 +380,8 @@ def pmc_counters(model, sd, args, names, timeout=150):
                     if busy is not None and gui:
                         # per SIMD: busy cycles / (1024 SIMDs x dispatch cycles per XCD)
                         res[n]["mfma_busy"] = busy / (1024.0 * gui / 8.0)
-                elif tag == "clock":
-                    gui = _per_launch(agg, n, "GRBM_GUI_ACTIVE")
-                    ms = (child or {}).get("kernels", {}).get(n, {}).get("ms")
-                    if gui and ms:
-                        res[n]["held_clock_ghz"] = gui / 8.0 / (ms * 1e-3) / 1e9
-                        res[n]["held_clock_batch"] = batch
+                    if v is None:
+                        errors.append(f"{tag}: no counter row matched launch {n}")
     finally:
         os.unlink(spec_file)
     for n in names:
@@ -435,10 +486,16 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        # every rank's own step time (the spread separates slow ranks from the
+        # collective), then the max over ranks for the metric
+        tdev = dev if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rank_ms = [a.item() / args.steps * 1e3 for a in allt]
+        elapsed = max(a.item() for a in allt)
     images = world * B * args.steps
     value = images / elapsed
 
@@ -467,17 +524,40 @@ def main():
                    "bound": "hbm" if n in HBM_BOUND else "mfma"}
         kern[n]["frac"] = (kern[n]["gbs"] / PEAK_HBM_GBS if n in HBM_BOUND
                            else kern[n]["tops"] / PEAK_INT8_TOPS)
+    # N > 1: the logits all-gather on its own (HIP events on the launch stream
+    # around a blocking all_gather_into_tensor of this batch's logits: the
+    # collective's latency as the timed step would see it if nothing hid it)
+    gather = None
+    if world > 1:
+        logits = model.run(x)
+        gms = []
+        for _ in range(max(3, min(args.steps, 20))):
+            barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            qd.gather_logits(logits, gathered[0])
+            e1.record()
+            torch.cuda.synchronize()
+            gms.append(e0.elapsed_time(e1))
+        gather = {"ms_mean": float(np.mean(gms)), "ms_min": float(np.min(gms)),
+                  "bytes_per_rank": int(logits.numel() * logits.element_size()),
+                  "note": "blocking all_gather_into_tensor of one batch's fp32 logits, HIP events "
+                          "on the launch stream; in the timed step it runs asynchronously behind "
+                          "the next batch's forward"}
     dom = max(names, key=lambda n: kern[n]["ms"])
     k = kern[dom]
     if k["bound"] == "mfma":
         roof = {"kernel": dom, "bound": "mfma", "achieved": k["tops"], "peak": PEAK_INT8_TOPS,
                 "unit": "TFLOP/s", "frac": k["frac"], "traffic": None,
-                "note": "int8 TOPS reported in the TFLOP/s slot; achieved = 2*MAC*1024 / mean HIP-event duration"}
+                "note": f"int8 TOPS reported in the TFLOP/s slot; achieved = 2*MAC*{B} / mean HIP-event duration"}
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": k["gbs"], "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": k["frac"], "traffic": None}
     pmc_err = "skipped (--no-pmc or N > 1)"
-    if rank == 0 and world == 1 and not args.no_pmc:
+    if rank == 0 and world == 1 and not args.no_pmc and under_profiler():
+        pmc_err = ("skipped: this run is itself under rocprofv3 (LD_PRELOAD / ROCPROF* env), "
+                   "so no nested counter passes are started")
+    elif rank == 0 and world == 1 and not args.no_pmc:
         pmc, pmc_err = pmc_counters(model, sd, args, names)
         for n in names:
             kern[n].update({kk: vv for kk, vv in pmc[n].items() if vv is not None})
@@ -488,9 +568,6 @@ def main():
                                 f"algorithmic bytes per launch {BYTES_PER_IMAGE[dom] * B}")
         if p.get("mfma_busy") is not None:
             roof["mfma_busy"] = p["mfma_busy"]
-        if p.get("held_clock_ghz"):
-            roof["held_clock_ghz"] = p["held_clock_ghz"]
-            roof["frac_at_held_clock"] = roof["achieved"] / (PEAK_INT8_TOPS * p["held_clock_ghz"] / 2.4)
     if pmc_err:
         roof["pmc_error"] = pmc_err
 
@@ -510,6 +587,10 @@ def main():
         "kernels": {n: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in kern[n].items()}
                     for n in names},
     }
+    if world > 1:
+        result["rank_ms_per_step"] = rank_ms
+        result["rank_ms_spread"] = max(rank_ms) - min(rank_ms)
+        result["allgather"] = gather
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baselines(sd, model, args.cpu_seconds)
         result["cpu_baseline"] = cb["static_ptq"]

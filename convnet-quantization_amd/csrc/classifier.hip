@@ -3,9 +3,12 @@
 // launches instead of two full GEMM kernels:
 //
 //  1. fc_splitk_kernel: fc1's u8 x s8 GEMM (M = batch, K = 4096, N = 512) split
-//     four ways along K.  A workgroup owns a 128 (rows) x 64 (features) tile of
-//     one K quarter; its four waves each compute 64 x 32 with
-//     v_mfma_i32_32x32x32_i8 straight from global memory.  Both operands are
+//     four ways along K.  From 1024 rows up a workgroup owns a 128 (rows) x 64
+//     (features) tile of one K quarter and its four waves each compute 64 x 32
+//     (fc_splitk_kernel<64>); below 1024 rows workgroups own 64 x 64 tiles and
+//     each wave 32 x 32 (fc_splitk_kernel<32>: twice the workgroups, so a
+//     small batch still fills the CUs).  Both on v_mfma_i32_32x32x32_i8
+//     straight from global memory.  Both operands are
 //     chunk-major ([K/32][rows][32]: conv6 writes its output that way, the
 //     weights are packed so at upload), so every fragment load is one
 //     contiguous 1 KB — row-major operands (4 KB row stride) ran 2-3x slower.

@@ -19,7 +19,7 @@
 // Numerics (oracle/qref.py resnet_qdq_forward, pinned to torch.ao by
 // tests/golden/net_resnet_qdq.npz): dequantize fp32(q - z) * s; BN eval
 // y = fmaf(x, alpha, beta) with alpha / beta from ATen's eval constants
-// (host, qconvnet/quant.py bn_eval_constants); ReLU keeps -0.0 like
+// (host, qconvnet/quant.py bn_eval_affine); ReLU keeps -0.0 like
 // torch.relu; quantize zp + rint(x * fp32(1/s)) clamped; avg-pool a
 // sequential fp32 sum in row-major window order, then / (H*W).  All NHWC,
 // channel innermost, 4 channels per lane (C % 4 == 0).

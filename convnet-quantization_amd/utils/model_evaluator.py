@@ -30,8 +30,10 @@ class ModelEvaluator:
         self.device = device
 
     def _place(self, model):
-        """(model, input device) as the reference places them: quantized models
-        on the CPU side of the boundary (:78-84), others on self.device."""
+        """(model, input device): every model goes to self.device.  The reference
+        forces quantized models to the CPU (:78-84) because fbgemm runs there;
+        our int8 models compute on the GPU, and with self.device == "cpu" they
+        take host tensors and keep their compute on the GPU (model.cpu())."""
         model.eval()
         if str(self.device) == "cpu":
             return model.cpu(), torch.device("cpu")

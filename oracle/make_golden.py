@@ -579,10 +579,65 @@ def _resnet_qdq_spec_from_torchao(q):
     return spec
 
 
+def reference_resnet_qdq(fp, calib_batches, per_channel=True):
+    """The reference's OWN CustomQuantizedResNet50 / CustomQuantizedBottleneck
+    (/root/reference/models/custom_quantization_model.py:60-143), imported
+    read-only from /root/reference, wrapped around a copy of the same ResNetRef
+    and converted the way torch.ao eager converts RefQDQResNet: a qconfig on
+    every CustomQuantizedConv2d / CustomQuantizedLinear (their QuantStub ->
+    op -> DeQuantStub run live), MinMax calibration on the same batches, then
+    convert.  The outer QuantStub / DeQuantStub (:107-108) carry no qconfig
+    and stay identities, as in RefQDQResNet.
+
+    That module imports torchvision at the top (:4) and never uses it; the
+    wheel is not installed here, so an empty module object stands in for it
+    during the import.  The reference's `models` package is
+    imported under its own name and removed from sys.modules afterwards."""
+    import copy
+    import types
+    import torch.nn as nn
+    import torch.ao.quantization as tq
+    saved = {k: v for k, v in sys.modules.items() if k == "models" or k.startswith("models.")}
+    for k in saved:
+        del sys.modules[k]
+    stub = "torchvision" not in sys.modules
+    if stub:
+        sys.modules["torchvision"] = types.ModuleType("torchvision")
+    sys.path.insert(0, "/root/reference")
+    try:
+        from models.custom_quantization_model import (CustomQuantizedConv2d, CustomQuantizedLinear,
+                                                      CustomQuantizedResNet50)
+    finally:
+        sys.path.pop(0)
+        for k in [k for k in sys.modules if k == "models" or k.startswith("models.")]:
+            del sys.modules[k]
+        sys.modules.update(saved)
+        if stub:
+            del sys.modules["torchvision"]
+    net = copy.deepcopy(fp).eval()
+    for li in range(1, 5):   # torchvision Bottleneck attributes the wrapper reads (:63-71)
+        for b in getattr(net, f"layer{li}"):
+            b.relu = nn.ReLU()
+            b.stride = b.conv2.stride[0]
+    torch.backends.quantized.engine = "fbgemm"
+    ref = CustomQuantizedResNet50(net).eval()
+    for m in ref.modules():
+        if isinstance(m, (CustomQuantizedConv2d, CustomQuantizedLinear)):
+            m.qconfig = tr.static_qconfig(per_channel)
+    tq.prepare(ref, inplace=True)
+    with torch.no_grad():
+        for xb in calib_batches:
+            ref(xb)
+    tq.convert(ref, inplace=True)
+    return ref.eval()
+
+
 def gen_resnet_qdq_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
     """§8(f)2 in the reference's own semantics: the same 1-1-1-1 ResNet at
     64x64 as CustomQuantizedResNet50 with live per-layer stubs
-    (torch_ref.RefQDQResNet, torch.ao eager, fbgemm, CPU calibration):
+    (torch_ref.RefQDQResNet, torch.ao eager, fbgemm, CPU calibration; asserted
+    equal, block by block and in the logits, to the reference's own
+    CustomQuantizedResNet50 built the same way — reference_resnet_qdq):
     fp32 BN / ReLU / max-pool / residual add / avg-pool between int8 convs.
     Stores every stub's and conv's qparams, int8-weight hashes, every conv's
     u8 output and every block's fp32 output by hash, the fc's u8 output and
@@ -619,6 +674,24 @@ def gen_resnet_qdq_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
         logits = q(torch.from_numpy(x)).numpy()
     for h in hooks:
         h.remove()
+    # pin the restatement to the reference's own classes: same fp32 net, same
+    # calibration -> every block's fp32 output and the logits bit for bit
+    ref = reference_resnet_qdq(fp, [torch.from_numpy(calib)])
+    ref_outs, hooks = {}, []
+    bi = 0
+    for li in range(1, 5):
+        for blk in getattr(ref, f"layer{li}"):
+            hooks.append(blk.register_forward_hook(
+                lambda m, a, o, key=f"block{bi}": ref_outs.__setitem__(key, o)))
+            bi += 1
+    with torch.no_grad():
+        ref_logits = ref(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    assert ref_logits.dtype == logits.dtype and (ref_logits == logits).all(), \
+        "RefQDQResNet differs from the reference's CustomQuantizedResNet50"
+    for k, t in ref_outs.items():
+        assert torch.equal(t, outs[k]), f"{k}: RefQDQBottleneck differs from CustomQuantizedBottleneck"
     spec = _resnet_qdq_spec_from_torchao(q)
     mine, inter = qref.resnet_qdq_forward(x, spec, keep=True)
     nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().numpy()  # noqa: E731

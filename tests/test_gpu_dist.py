@@ -132,3 +132,8 @@ def test_bench_two_ranks_rehearsal(dev):
     assert res[1] is None   # one JSON line, from rank 0
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 512 and d["value"] > 0
     assert d["config"]["collective"]
+    # compute vs collective: every rank's step time and the all-gather's own time
+    assert len(d["rank_ms_per_step"]) == 2 and all(t > 0 for t in d["rank_ms_per_step"])
+    assert d["rank_ms_spread"] >= 0
+    assert abs(d["ms_per_step"] - max(d["rank_ms_per_step"])) < 1e-6
+    assert d["allgather"]["ms_mean"] > 0 and d["allgather"]["bytes_per_rank"] == 256 * 10 * 4

@@ -320,7 +320,8 @@ def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
     from types import SimpleNamespace as NS
     from qconvnet import ops, quant as Q
     rng = np.random.default_rng(7 + zx)
-    m, k, n1, n2 = 256, 4096, 512, 10
+    # 896 rows: below 1024 the split-K runs 64-row workgroups (fc_splitk_kernel<32>)
+    m, k, n1, n2 = 896, 4096, 512, 10
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     qx = rng.integers(0, 256, (m, k), dtype=np.uint8)
     w1 = rng.integers(-128, 128, (n1, k), dtype=np.int8)
@@ -350,7 +351,7 @@ def test_classifier_head_equals_two_linears(dev, per_channel, zx, z1, z2):
     assert torch.equal(y2, y2_ref)
     assert torch.equal(y2f, y2f_ref)
     # the workspace is reusable across launches and batch sizes
-    for mm in (m, 128, m, m):
+    for mm in (m, 128, 384, 640, m):
         y2.zero_()
         y2f.zero_()
         assert ops.classifier(ops.to_kmajor(T(qx[:mm])), l1, l2, ws, y1[:mm], y2[:mm], y2f[:mm])
