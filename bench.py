@@ -349,6 +349,26 @@ def _per_launch(agg, launch, counter):
     return tot if seen else None
 
 
+def clock_pass(spec_file, args, mode, timeout=240):
+    """The in-kernel clock of the conv launches: tools/clock_probe.py as a plain
+    child process (no profiler) on the diagnostic library with stamped copies
+    of the conv kernels, same model and batch.  Returns {launch: {...}}."""
+    probe = os.path.join(ROOT, "tools", "clock_probe.py")
+    lib = os.path.join(ROOT, "tools", "clock", "libqconvnet_clock.so")
+    if not os.path.exists(lib):
+        raise RuntimeError("tools/clock/libqconvnet_clock.so not built (__graft_entry__.build())")
+    cmd = [sys.executable, probe, "--batch", str(args.batch), "--spec-file", spec_file,
+           "--workload", "qdq" if mode != "static" else "convnet"]
+    p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    if p.returncode != 0:
+        raise RuntimeError(f"clock probe exit {p.returncode}: {p.stderr[-400:]}")
+    line = next((ln for ln in p.stdout.splitlines() if ln.startswith("{")), None)
+    if line is None:
+        raise RuntimeError("clock probe printed no JSON line")
+    return json.loads(line)["kernels"]
+
+
 def pmc_counters(model, sd, args, names, timeout=150):
     """Counter passes for every launch; returns ({launch: {...}}, error text)."""
     fd, spec_file = tempfile.mkstemp(prefix="qcn_spec_", suffix=".pt", dir="/tmp")
@@ -382,6 +402,16 @@ def pmc_counters(model, sd, args, names, timeout=150):
                         res[n]["mfma_busy"] = busy / (1024.0 * gui / 8.0)
                     if v is None:
                         errors.append(f"{tag}: no counter row matched launch {n}")
+        try:
+            clk = clock_pass(spec_file, args, model.mode)
+            for n in names:
+                c = clk.get(n, {})
+                if "clock_ghz" in c:
+                    res[n]["clock_ghz"] = c["clock_ghz"]
+                    res[n]["mfma_issue_at_clock"] = c["mfma_issue_at_clock"]
+                    res[n]["clock_probe_ms"] = c["ms"]
+        except Exception as e:
+            errors.append(f"clock: {e}")
     finally:
         os.unlink(spec_file)
     for n in names:
@@ -568,6 +598,12 @@ def main():
                                 f"algorithmic bytes per launch {BYTES_PER_IMAGE[dom] * B}")
         if p.get("mfma_busy") is not None:
             roof["mfma_busy"] = p["mfma_busy"]
+        if p.get("clock_ghz"):
+            # the clock the chip holds in this kernel (in-kernel s_memtime /
+            # s_memrealtime of a stamped diagnostic copy after >= 2 s of back-to-back
+            # forwards, tools/clock_probe.py) and the MFMA issue fraction at it
+            roof["clock_ghz_in_kernel"] = p["clock_ghz"]
+            roof["mfma_issue_at_clock"] = roof["frac"] * 2.4 / p["clock_ghz"]
     if pmc_err:
         roof["pmc_error"] = pmc_err
 

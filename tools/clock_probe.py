@@ -1,0 +1,126 @@
+"""In-kernel clock of the SimpleConvNet conv launches (diagnostic, not product).
+
+Loads tools/clock/libqconvnet_clock.so (QCN_LIB) — the product library with
+the three conv launches replaced by stamped copies of the same kernels — runs
+the bench's forward back to back for >= 2 s (MI355X_MICROARCH.md 'DVFS
+give-back' item 6), then K more steps with HIP events between launches, and
+reads the last launch's per-workgroup stamps:
+
+    clock  = (s_memtime delta) / (s_memrealtime delta) x 100 MHz, median over workgroups
+    issue  = frac_at_2.4GHz x 2.4 / clock   (MFMA issue fraction at the held clock)
+
+    python tools/clock_probe.py [--batch 1024] [--workload convnet|qdq] [--spec-file F]
+
+Prints one JSON line.  bench.py runs it as a child with the parent's model.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG_LIB = os.path.join(ROOT, "tools", "clock", "libqconvnet_clock.so")
+os.environ["QCN_LIB"] = DIAG_LIB   # before qconvnet is imported
+for _p in (os.path.join(ROOT, "convnet-quantization_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import ctypes  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+KINDS = {"conv12": 0, "conv34": 1, "conv56": 2}
+MFMA_MAC_PER_CLK_SIMD = 1024   # v_mfma_i32_32x32x32_i8: 32768 MAC per 32 cycles
+
+
+def grid_of(name, n, ncu):
+    if name == "conv12":
+        return min(n, ncu)
+    if name == "conv34":
+        return n                       # one 16x16 image (256 pixels) per 4-wave workgroup
+    return (n * 64 + 127) // 128 if n < 4 * ncu else (n * 64 + 255) // 256
+
+
+def main():
+    import bench
+    from qconvnet import _lib, data
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--workload", choices=("convnet", "qdq"), default="convnet")
+    ap.add_argument("--spec-file", default=None)
+    ap.add_argument("--heat-s", type=float, default=2.5)
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    B = args.batch or (1024 if args.workload == "convnet" else 256)
+    lib = _lib.load()
+    assert os.path.samefile(_lib.LIB_PATH, DIAG_LIB), "the diagnostic library must be the one loaded"
+    fn = lib.qcn_clock_read
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    mode = "qdq" if args.workload == "qdq" else "static"
+    model, _ = bench.build_model(0, dev, False, args.spec_file, mode)
+    x = torch.from_numpy(data.synthetic_images(B, 100)).to(dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+
+    # heat: >= heat_s of back-to-back forwards
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        model.run(x)
+        k += 1
+        if k % 50 == 0:
+            torch.cuda.synchronize()
+            if time.perf_counter() - t0 >= args.heat_s:
+                break
+    names = model.kernel_names(x.shape)
+    per = {n: [] for n in names}
+    for _ in range(args.steps):
+        m = []
+        model.run(x, marks=m)
+        for i, n in enumerate(names):
+            per[n].append(m[i])
+            per[n].append(m[i + 1])
+    torch.cuda.synchronize()
+    out = {"batch": B, "workload": args.workload, "heat_s": time.perf_counter() - t0,
+           "heat_steps": k, "kernels": {}}
+    for n in names:
+        evs = per[n]
+        ms = float(np.mean([evs[2 * i].elapsed_time(evs[2 * i + 1]) for i in range(len(evs) // 2)]))
+        rec = {"ms": ms}
+        if n in KINDS:
+            g = grid_of(n, B, ncu)
+            buf = np.zeros((g, 4), np.uint64)
+            _lib.check(fn(KINDS[n], buf.ctypes.data, g), "qcn_clock_read")
+            t0_, t1_, r0_, r1_ = (buf[:, i].astype(np.float64) for i in range(4))
+            cyc, rt = t1_ - t0_, r1_ - r0_
+            ok = rt > 0
+            ghz = cyc[ok] / rt[ok] * 0.1
+            frac = 2.0 * bench.MAC_PER_IMAGE[n] * B / (ms * 1e-3) / 1e12 / bench.PEAK_INT8_TOPS
+            clock = float(np.median(ghz))
+            # MFMA cycles per SIMD of one workgroup (its images' MACs over its 4 SIMDs)
+            img_per_wg = B / g
+            mfma_cyc_wg = bench.MAC_PER_IMAGE[n] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)
+            rec.update({"clock_ghz": clock, "clock_ghz_p10": float(np.percentile(ghz, 10)),
+                        "clock_ghz_p90": float(np.percentile(ghz, 90)),
+                        "workgroups": int(g), "wg_cycles_median": float(np.median(cyc[ok])),
+                        "wg_mfma_cycles_per_simd": mfma_cyc_wg,
+                        "launch_span_us": float((r1_.max() - r0_.min()) / 100.0),
+                        "frac_at_2p4": frac, "mfma_issue_at_clock": frac * 2.4 / clock})
+        out["kernels"][n] = rec
+    print(json.dumps(out))
+    for n, r in out["kernels"].items():
+        if "clock_ghz" in r:
+            print(f"# {n}: {r['ms'] * 1e3:.1f} us, clock {r['clock_ghz']:.3f} GHz "
+                  f"(p10 {r['clock_ghz_p10']:.3f}, p90 {r['clock_ghz_p90']:.3f}), frac@2.4 "
+                  f"{r['frac_at_2p4']:.3f}, MFMA issue at the held clock {r['mfma_issue_at_clock']:.3f}, "
+                  f"WG {r['wg_cycles_median']:.0f} cyc vs {r['wg_mfma_cycles_per_simd']:.0f} MFMA cyc/SIMD",
+                  file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
