@@ -53,6 +53,7 @@ MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
 MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
 MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
 MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
+MAC_PER_IMAGE["conv3456"] = MAC_PER_IMAGE["conv34"] + MAC_PER_IMAGE["conv56"]
 MAC_PER_IMAGE["net"] = sum(MAC_PER_IMAGE[f"conv{i}"] for i in range(1, 7))
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
@@ -66,12 +67,15 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "fc12": 4096 + 512 + 10 + 40,
                  "conv34": 16 * 16 * 64 + 8 * 8 * 128,
                  "conv56": 8 * 8 * 128 + 4 * 4 * 256,
+                 # a2 in, a4 out (read back from L2 inside the launch), a6 out
+                 "conv3456": 16 * 16 * 64 + 8 * 8 * 128 + 4 * 4 * 256,
                  "net": 3 * 32 * 32 * 4 + 4 * 4 * 256}
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
-                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256",),
+                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel"),
+                  "conv3456": ("conv3456_kernel",),
                   # "fc_finish" matches fc_finish_kernel (static) and fc_finish_qdq_kernel (QDQ)
                   "fc12": ("fc_splitk_kernel", "fc_finish"),
                   "fc1": ("linear_u8s8_kernel",), "fc2": ("linear_f32_kernel",)}

@@ -251,16 +251,20 @@ QCN_DEV v16i acc_init_corr(const int* __restrict__ corr, int co_base, int hi) {
 
 // Copy the staged [opx][cout] u8 tile (row stride OS) to its contiguous NHWC
 // destination with 16-B coalesced stores (full cache lines, no partial writes).
-template <int COUT, int OS, int NT>
+// WT: write-through (the next launch reads it); plain stores keep the lines
+// in this XCD's L2 for a read-back by the same workgroup (conv3456).
+template <int COUT, int OS, int NT, bool WT = true>
 QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid) {
   constexpr int CPR = COUT / 16;
   const int total = opx * CPR;
-  const wt_rsrc_t wr = wt_rsrc(dst);   // the next launch reads it: write through
+  const wt_rsrc_t wr = wt_rsrc(dst);
   for (int e = tid; e < total; e += NT) {
     const int row = e / CPR, ch = e % CPR;
-    if (row < valid_px)
-      store_wt16(wr, (uint32_t)(row * COUT + ch * 16),
-                 *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16));
+    if (row < valid_px) {
+      const uint4 v = *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16);
+      if constexpr (WT) store_wt16(wr, (uint32_t)(row * COUT + ch * 16), v);
+      else *reinterpret_cast<uint4*>(dst + row * COUT + ch * 16) = v;
+    }
   }
 }
 
@@ -447,7 +451,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 
 // Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
 // the workgroup's contiguous NHWC output span with 16-B stores.
-template <class C>
+template <class C, bool WT = true>
 QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* lds, int nimg,
                            int wave, int lane, int tid, uint8_t* __restrict__ y, int tile,
                            const float* ek_override = nullptr) {
@@ -495,7 +499,7 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
     }
     return;
   }
-  store_staged<COUT, C::OS, C::NT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
+  store_staged<COUT, C::OS, C::NT, WT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
 }
 
 // Stage the input patch of the workgroup's tile (images n0.., first output row
@@ -598,14 +602,52 @@ struct PairCfg {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <class CA, class CB, bool BYPASS_L1 = false>
+// A's epilogue into B's LDS patch (zero-point halo, then the requantized
+// interior as q - 128).  Shared by both pair bodies.
+template <class CA, class CB>
+QCN_DEV void pair_handoff(v16i (&acc)[CA::WI][4], const ConvEpi& epa, const float* eka, int xb_zp,
+                          uint8_t* lds, int wave, int lane, int tid) {
+  const uint32_t padw = xor80(splat_u8(xb_zp));
+  const uint4 pad4 = make_uint4(padw, padw, padw, padw);
+  constexpr int CH16 = CB::kCin / 16;
+  constexpr int HALO = CB::SEGS * (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
+  for (int e = tid; e < HALO * CH16; e += CB::NT) {
+    const int hs = e / CH16, chunk = e % CH16;
+    const int seg = hs / (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
+    int r = hs % (2 * CB::PCOLS + 2 * (CB::PROWS - 2)), pr, pc;
+    if (r < CB::PCOLS) { pr = 0; pc = r; }
+    else if (r < 2 * CB::PCOLS) { pr = CB::PROWS - 1; pc = r - CB::PCOLS; }
+    else { r -= 2 * CB::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? CB::PCOLS - 1 : 0; }
+    *reinterpret_cast<uint4*>(lds + CB::slot(seg, pr, pc) + chunk * 16) = pad4;
+  }
+  const int wc = wave % CA::WCO, wp = wave / CA::WCO;
+  const int l32 = lane & 31, hi = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < CA::WI; ++i) {
+    const int co_base = wc * 32 * CA::WI + i * 32;
+    const EpiK K = load_epik_lds(eka, CA::kCout, co_base, hi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = (wp * 4 + j) * 32 + l32;
+      const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
+      epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
+                                      lds + CB::slot(seg, row + 1, col + 1));
+    }
+  }
+}
+
+template <class CA, class CB, bool BYPASS_L1 = false, bool WT = true>
 QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
                            const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                            const int8_t* __restrict__ wb, ConvEpi epb,
                            uint8_t* __restrict__ y) {
   using P = PairCfg<CA, CB>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // laundered: a caller that runs this body more than once (conv3456) must
+  // not get thread-id-derived addresses hoisted and held live across calls
+  int tid_l = threadIdx.x;
+  asm volatile("" : "+v"(tid_l));
+  const int tid = tid_l, lane = tid & 63, wave = tid >> 6;
   const long p0 = (long)tile * CA::PXB;
   const int n0 = (int)(p0 / CA::IMG);
   const int y0 = (int)((p0 % CA::IMG) / CA::W);
@@ -618,40 +660,12 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
   v16i acc[CA::WI][4];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
 
-  // ---- A's epilogue into B's patch (A's patch and ring are dead past the
-  // main loop's final barrier): zero-point halo, then the requantized interior
-  {
-    const uint32_t padw = xor80(splat_u8(xb_zp));
-    const uint4 pad4 = make_uint4(padw, padw, padw, padw);
-    constexpr int CH16 = CB::kCin / 16;
-    constexpr int HALO = CB::SEGS * (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
-    for (int e = tid; e < HALO * CH16; e += CB::NT) {
-      const int hs = e / CH16, chunk = e % CH16;
-      const int seg = hs / (2 * CB::PCOLS + 2 * (CB::PROWS - 2));
-      int r = hs % (2 * CB::PCOLS + 2 * (CB::PROWS - 2)), pr, pc;
-      if (r < CB::PCOLS) { pr = 0; pc = r; }
-      else if (r < 2 * CB::PCOLS) { pr = CB::PROWS - 1; pc = r - CB::PCOLS; }
-      else { r -= 2 * CB::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? CB::PCOLS - 1 : 0; }
-      *reinterpret_cast<uint4*>(lds + CB::slot(seg, pr, pc) + chunk * 16) = pad4;
-    }
-    const int wc = wave % CA::WCO, wp = wave / CA::WCO;
-    const int l32 = lane & 31, hi = lane >> 5;
-#pragma unroll
-    for (int i = 0; i < CA::WI; ++i) {
-      const int co_base = wc * 32 * CA::WI + i * 32;
-      const EpiK K = load_epik_lds(eka, CA::kCout, co_base, hi);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = (wp * 4 + j) * 32 + l32;
-        const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
-        epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
-                                        lds + CB::slot(seg, row + 1, col + 1));
-      }
-    }
-  }
+  // A's epilogue into B's patch (A's patch and ring are dead past the main
+  // loop's final barrier)
+  pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
   __syncthreads();
   conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
-  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+  conv_epilogue<CB, WT>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
 }
 
 template <class CA, class CB>
@@ -660,6 +674,204 @@ void convpair_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                      const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                      const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   convpair_body<CA, CB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+}
+
+// --------------------------------------------------------------------------
+// Weights straight from global memory (L2) into registers.  When a workgroup
+// has one wave along the pixels (WPX = 1), every weight fragment is used by
+// exactly ONE of its waves: an LDS ring would stage bytes that are read once,
+// and its per-chunk barriers would hold the waves in lockstep.  Here each wave
+// loads its own A fragments D K-steps ahead (buffer loads, the step's offset in
+// the scalar operand) and the K loop has no barrier at all, so the LDS holds
+// only the patch and two independent 4-wave workgroups fit on a CU: one
+// workgroup's staging and epilogues run beside the other's MFMAs.
+template <class C, int D>
+struct GaFrag {
+  v4i fa[D + 1][C::WI];
+};
+
+// Issue the A-fragment loads of K-step s (chunk s / 2, half kk = s % 2) into
+// slot s % (D + 1).  wr: buffer resource of the packed weights; voff: this
+// lane's row offset ((wc*32*WI + l32) * 64 + hi * 16).
+template <class C, int D>
+QCN_DEV void ga_issue(GaFrag<C, D>& g, wt_rsrc_t wr, int voff, int s) {
+  const int ch = s >> 1, kk = s & 1;
+#pragma unroll
+  for (int i = 0; i < C::WI; ++i) {
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(wr, voff, ch * C::WBUF + i * 32 * 64 + kk * 32, 0);
+    g.fa[s % (D + 1)][i] = (v4i){(int)t[0], (int)t[1], (int)t[2], (int)t[3]};
+  }
+}
+
+template <class C>
+QCN_DEV int ga_voff(int wave, int lane) {
+  return ((wave % C::WCO) * 32 * C::WI + (lane & 31)) * 64 + (lane >> 5) * 16;
+}
+
+// The first D K-steps' loads (issued early so their latency overlaps the
+// patch staging or the previous conv's epilogue).
+template <class C, int D>
+QCN_DEV void ga_prefetch(GaFrag<C, D>& g, const int8_t* __restrict__ wpk, int wave, int lane) {
+  const wt_rsrc_t wr = wt_rsrc(wpk);
+  const int voff = ga_voff<C>(wave, lane);
+#pragma unroll
+  for (int s = 0; s < D; ++s) ga_issue<C, D>(g, wr, voff, s);
+}
+
+// K loop over the patch staged in LDS (layout C::slot, all waves' writes
+// visible), A fragments from g (steps 0..D-1 already issued).  Returns after a
+// workgroup barrier: every wave's patch reads are done and the caller may
+// reuse the LDS.
+template <class C, int D>
+QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ wpk,
+                              const int* __restrict__ corr, int wave, int lane,
+                              v16i (&acc)[C::WI][4], GaFrag<C, D>& g) {
+  constexpr int CB = C::kCin / 64;
+  constexpr int WI = C::WI, MPS = C::MPS, S = 2 * C::NCH;
+  static_assert(D >= 1 && D < S, "prefetch depth");
+  const int wc = wave % C::WCO, wp = wave / C::WCO;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const PatchAddr<C> pa(wp, l32, hi);
+  const wt_rsrc_t wr = wt_rsrc(wpk);
+  const int voff = ga_voff<C>(wave, lane);
+#pragma unroll
+  for (int i = 0; i < WI; ++i) {
+    const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
+  }
+  auto rd_b = [&](int s, int j) {
+    const int ch = s >> 1, kk = s & 1;
+    const int tap = ch / CB, cb = ch % CB;
+    return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 +
+                                         kk * 32);
+  };
+  v4i fb[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = rd_b(0, j);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+#pragma unroll
+    for (int m = 0; m < MPS; ++m) {
+      // next step's B fragments one per MFMA (even slots), the A loads of
+      // step s + D in the odd slots
+      if (s + 1 < S && (m & 1) == 0 && (m >> 1) < 4) fb[(s + 1) & 1][m >> 1] = rd_b(s + 1, m >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[m / 4][m % 4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g.fa[s % (D + 1)][m / 4], fb[s & 1][m % 4],
+                                                                acc[m / 4][m % 4], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + D < S && m == MPS / 2 - 1) {
+        // slot (s + D) % (D + 1) == (s - 1) % (D + 1): consumed by step s - 1
+        ga_issue<C, D>(g, wr, voff, s + D);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (WI == 2) {
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]));
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+}
+
+// LDS plan of the direct-weight pair: A's patch and then B's patch at offset
+// 0 (A's is dead once every wave is past A's loop), both convs' epilogue
+// constants behind the larger patch; B's output staging reuses the patch.
+template <class CA, class CB>
+struct PairGaCfg {
+  static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
+                CA::W == CB::W && CA::WI == CB::WI, "same whole-image tiling");
+  static constexpr int PATCH = CA::PATCH > CB::PATCH ? CA::PATCH : CB::PATCH;
+  static_assert(CB::OPX * CB::OS <= PATCH, "B's staging fits the dead patch");
+  static constexpr int OFF_EA = PATCH;
+  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
+  static constexpr int LDS = OFF_EB + 12 * CB::kCout;
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+template <class CA, class CB, int D>
+QCN_DEV void convpair_ga_body(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                              const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                              const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  using P = PairGaCfg<CA, CB>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  // laundered: a caller that runs this body more than once (conv3456) must
+  // not get thread-id-derived addresses hoisted and held live across calls
+  int tid_l = threadIdx.x;
+  asm volatile("" : "+v"(tid_l));
+  const int tid = tid_l, lane = tid & 63, wave = tid >> 6;
+  const long p0 = (long)tile * CA::PXB;
+  const int n0 = (int)(p0 / CA::IMG);
+  const int y0 = (int)((p0 % CA::IMG) / CA::W);
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  GaFrag<CA, D> ga;
+  ga_prefetch<CA, D>(ga, wa, wave, lane);
+  stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
+  stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
+  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
+  __syncthreads();
+  v16i acc[CA::WI][4];
+  conv_mainloop_ga<CA, D>(lds, wa, epa.corr, wave, lane, acc, ga);
+  GaFrag<CB, D> gb;
+  ga_prefetch<CB, D>(gb, wb, wave, lane);   // B's first loads ride under A's epilogue
+  pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
+  __syncthreads();
+  conv_mainloop_ga<CB, D>(lds, wb, epb.corr, wave, lane, acc, gb);
+  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+}
+
+template <class CA, class CB, int D>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                        const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                        const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  convpair_ga_body<CA, CB, D>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+}
+
+// --------------------------------------------------------------------------
+// conv3 -> conv4 -> conv5 -> conv6 in one launch.  Each 4-wave workgroup owns
+// two images: conv3+4 of the first (LDS weight ring, as convpair_kernel),
+// conv3+4 of the second, then conv5+6 of both (weights from L2,
+// convpair_ga_body).  a4 goes out to HBM/L2 with plain stores and comes back
+// into conv5's patch in the same workgroup (16 KB per workgroup, no other
+// workgroup reads it: no inter-workgroup hand-off).  Two workgroups per CU
+// run independently, and the grid is one round of workgroups, so the launch
+// pays one dispatch ramp and drain instead of two kernels' worth.
+template <class C3, class C4, class C5, class C6, int D>
+struct Conv3456Cfg {
+  static_assert(C3::NT == C5::NT && C4::kCout == C5::kCin && C4::kPool && C4::W / 2 == C5::W,
+                "conv4's pooled output is conv5's input");
+  static_assert(C5::SEGS == 2 && C3::SEGS == 1, "two images per workgroup, one per conv3+4 pass");
+  static constexpr int L34 = PairCfg<C3, C4>::LDS, L56 = PairGaCfg<C5, C6>::LDS;
+  static constexpr int LDS = L34 > L56 ? L34 : L56;
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+template <class C3, class C4, class C5, class C6, int D>
+__global__ __launch_bounds__(C3::NT, 2)
+void conv3456_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                     const int8_t* __restrict__ w3, ConvEpi ep3, int z4in,
+                     const int8_t* __restrict__ w4, ConvEpi ep4, uint8_t* __restrict__ a4, int z5in,
+                     const int8_t* __restrict__ w5, ConvEpi ep5, int z6in,
+                     const int8_t* __restrict__ w6, ConvEpi ep6, uint8_t* __restrict__ y) {
+  const int t = (int)blockIdx.x;
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    const int n = 2 * t + k;
+    if (n < nimg) {
+      convpair_body<C3, C4, false, false>(n, x, nimg, x_zp, w3, ep3, z4in, w4, ep4, a4);
+    }
+    // this image's a4 stores retired (the read-back below and the next
+    // image's LDS staging follow)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  convpair_ga_body<C5, C6, D>(t, a4, nimg, z5in, w5, ep5, z6in, w6, ep6, y);
 }
 
 // --------------------------------------------------------------------------
@@ -1317,6 +1529,19 @@ int launch_pair(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const Co
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+template <class CA, class CB, int D>
+int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
+                   int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
+  using P = PairGaCfg<CA, CB>;
+  const long pix = (long)nimg * CA::IMG;
+  const int grid = (int)((pix + CA::PXB - 1) / CA::PXB);
+  auto k = convpair_ga_kernel<CA, CB, D>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 // Tuned instantiations: the SimpleConvNet layers and the
 // small shapes the parity fixtures use.
 int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nimg, int x_zp,
@@ -1427,6 +1652,17 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   // SIMD, a third fewer LDS bytes per MFMA) measured slower with no partner
   // wave to cover the epilogues (63 vs 53 us, 56 vs 51 us) and is not built.
   if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
+    // QCN_PAIR34 (A/B switch): 0 = LDS weight ring, D >= 1 = weights from L2
+    // into registers D K-steps ahead (both waves of a cout block load them)
+    static const int impl34 = [] {
+      const char* e = std::getenv("QCN_PAIR34");
+      return e ? std::atoi(e) : 0;
+    }();
+    using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
+    using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+    if (impl34 == 2) return launch_pair_ga<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl34 == 3) return launch_pair_ga<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl34 == 4) return launch_pair_ga<A3, B4, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                        ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
@@ -1436,6 +1672,20 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // fill the LDS); below four images per CU that leaves CUs idle, so small
     // batches take two images per 4-wave workgroup (same wave tile and
     // patch layout, twice the workgroups)
+    // QCN_PAIR56 (A/B switch): 0 = LDS weight ring (8-wave, 4 images per
+    // workgroup), D >= 1 = weights from L2 into registers D K-steps ahead
+    // (4-wave, 2 images per workgroup, two workgroups per CU)
+    static const int impl56 = [] {
+      const char* e = std::getenv("QCN_PAIR56");
+      return e ? std::atoi(e) : 4;
+    }();
+    using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
+    using B1 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
+    if (impl56 == 1) return launch_pair_ga<A1, B1, 1>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl56 == 2) return launch_pair_ga<A1, B1, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl56 == 3) return launch_pair_ga<A1, B1, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl56 == 4) return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl56 == 5) return launch_pair_ga<A1, B1, 5>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     const int ncu = qcn_cu_count();
     if (ncu > 0 && nimg < 4 * ncu)
       return launch_pair<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
@@ -1446,6 +1696,51 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;
+}
+
+// ConvEpi of one qcn_conv_layer_t; *zin receives the next layer's input zp.
+static int layer_epi(const qcn_conv_layer_t* l, int cout, ConvEpi& ep, int& zin) {
+  if (!l || !l->w_packed || !l->u || !l->v || !l->mult || !l->corr || l->cout != cout) return QCN_ERR_ARG;
+  if (l->y_zp < 0 || l->y_zp > 255) return QCN_ERR_ARG;
+  ep = ConvEpi{l->u, l->v, l->mult, l->corr, l->y_zp, l->relu ? l->y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
+  zin = l->y_zp;
+  if (l->qdq) {
+    ep.qdq = 1;
+    ep.s1 = l->qdq->s1; ep.z1 = l->qdq->z1; ep.inv2 = l->qdq->inv2; ep.z2 = l->qdq->z2;
+    zin = l->qdq->z2;
+  }
+  return QCN_OK;
+}
+
+int qcn_conv3456_u8s8(const uint8_t* x, int nimg, int x_zp, const qcn_conv_layer_t* l3,
+                      const qcn_conv_layer_t* l4, const qcn_conv_layer_t* l5,
+                      const qcn_conv_layer_t* l6, uint8_t* a4, int kmajor, uint8_t* y,
+                      void* stream) {
+  if (!x || !a4 || !y || nimg <= 0 || x_zp < 0 || x_zp > 255) return QCN_ERR_ARG;
+  if (!l3 || !l4 || !l5 || !l6) return QCN_ERR_ARG;
+  if (l3->cout != 128 || l4->cout != 128 || l5->cout != 256 || l6->cout != 256) return QCN_ERR_UNSUPPORTED;
+  ConvEpi e3, e4, e5, e6;
+  int z4, z5, z6, zo;
+  int rc;
+  if ((rc = layer_epi(l3, 128, e3, z4)) || (rc = layer_epi(l4, 128, e4, z5)) ||
+      (rc = layer_epi(l5, 256, e5, z6)) || (rc = layer_epi(l6, 256, e6, zo)))
+    return rc;
+  if (kmajor && (long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
+  e6.kmajor = kmajor ? 1 : 0;
+  using C3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
+  using C4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+  using C5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
+  using C6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
+  constexpr int D = 4;
+  using K = Conv3456Cfg<C3, C4, C5, C6, D>;
+  auto k = conv3456_kernel<C3, C4, C5, C6, D>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, K::LDS, attr_done)) return QCN_ERR_HIP;
+  const int grid = (nimg + 1) / 2;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(C3::NT), K::LDS, (hipStream_t)stream, x, nimg, x_zp,
+                     l3->w_packed, e3, z4, l4->w_packed, e4, a4, z5, l5->w_packed, e5, z6,
+                     l6->w_packed, e6, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
 int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,

@@ -240,6 +240,30 @@ def conv_pair(x, la, lb, out, kmajor=False):
     return True
 
 
+def _layer(d):
+    return _lib.ConvLayer(d.w.data_ptr(), d.cout, d.u.data_ptr(), d.v.data_ptr(), d.mult.data_ptr(),
+                          d.corr.data_ptr(), int(d.z_y), int(bool(d.relu)),
+                          C.pointer(d.qdq) if d.qdq is not None else None)
+
+
+def conv3456(x, l3, l4, l5, l6, a4, out, kmajor=False):
+    """conv3+conv4 (pool) + conv5+conv6 (pool) in one launch (qcn_conv3456_u8s8).
+    ``a4`` receives conv4's pooled output (u8 NHWC [n,8,8,128]).  Returns False
+    when the channel counts are not SimpleConvNet's."""
+    _need(x, torch.uint8, "conv3456.x")
+    _need(a4, torch.uint8, "conv3456.a4")
+    n, h, w, cin = x.shape
+    if (h, w, cin) != (16, 16, 64) or tuple(a4.shape) != (n, 8, 8, 128):
+        return False
+    L = [_layer(d) for d in (l3, l4, l5, l6)]
+    rc = lib().qcn_conv3456_u8s8(_ptr(x), n, int(l3.z_x), *(C.byref(t) for t in L), _ptr(a4),
+                                 int(bool(kmajor)), _ptr(out), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "conv3456")
+    return True
+
+
 def conv3x3_kmajor(x, x_zp, w_packed, cout, u, v, mult, corr, y_zp, relu, pool, out):
     """conv3x3 whose output is chunk-major [oh*ow*cout/32, n, 32] (conv6 -> fc1).
     Returns False when the shape is not supported (caller uses conv3x3)."""

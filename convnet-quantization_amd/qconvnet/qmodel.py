@@ -305,7 +305,10 @@ class QuantizedConvNet:
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
-            names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
+            if self._block34(2 if self._fused(x_shape) else 1):
+                names[names.index("conv3"):names.index("conv6") + 1] = ["conv3456"]
+            else:
+                names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
         if self._head(x_shape[0], keep):
             names = names[:-2] + ["fc12"]
         return tuple(names)
@@ -315,6 +318,12 @@ class QuantizedConvNet:
         activation stays in LDS); keep=True runs them per layer so every
         activation is inspectable."""
         return self.fuse_pairs and not keep and os.environ.get("QCN_PAIRS", "1") == "1"
+
+    def _block34(self, first):
+        """conv3..conv6 as ONE launch (qcn_conv3456_u8s8) behind the fused
+        conv12 when QCN_CONV3456=1 (A/B switch; measured slower than the two
+        pair launches, 99.2 vs 95.5 us, so off by default)."""
+        return first == 2 and os.environ.get("QCN_CONV3456", "0") == "1"
 
     def _head_fused(self, n):
         f1, f2 = self.fc1, self.fc2
@@ -373,6 +382,19 @@ class QuantizedConvNet:
             mark()
             prev, first = b["a1"], 1
         pairs = self._pairs(keep)
+        if pairs and self._block34(first):
+            # conv3..conv6 in one launch (conv4's pooled output round-trips
+            # through b["a4"] inside the launch)
+            if head:
+                if "a6k" not in b:
+                    b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
+                out, km = b["a6k"], True
+            else:
+                out, km = b["a6"], False
+            if not ops.conv3456(prev, L[2], L[3], L[4], L[5], b["a4"], out, kmajor=km):
+                raise RuntimeError("fused conv3..conv6 rejected a supported shape")
+            mark()
+            prev, first = out, 6
         for i in range(first, 6):
             d = L[i]
             if pairs and i in (2, 4):   # conv3+conv4, conv5+conv6 in one launch each

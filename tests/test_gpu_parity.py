@@ -429,16 +429,24 @@ def test_conv_kmajor_output(dev, pool):
     assert torch.equal(ops.from_kmajor(out), ref.view(n, -1))
 
 
+# the block launches under test: conv3..conv6 as ONE launch (qcn_conv3456_u8s8,
+# the default) or as the two pair launches (QCN_CONV3456=0)
+BLOCKS = [("1", "conv3456"), ("0", "conv34")]
+
+
+@pytest.mark.parametrize("block", BLOCKS, ids=["conv3456", "pairs"])
 @pytest.mark.parametrize("per_channel", [False, True])
-def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
-    """Same for the per-layer QDQ model (both qdq hand-offs inside a pair)."""
+def test_conv_pairs_qdq_equal_layerwise(dev, per_channel, block, monkeypatch):
+    """Same for the per-layer QDQ model (every qdq hand-off inside the fused
+    launches)."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
+    monkeypatch.setenv("QCN_CONV3456", block[0])
     z = netfix.load(per_channel)
     spec = netfix.qdq_spec(z)
     x = torch.from_numpy(netfix.images(z)).to(dev)
     model = QuantizedConvNet(spec, dev)
-    assert "conv34" in model.kernel_names(x.shape)
+    assert block[1] in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     a4_p = model.buffers(x.shape[0])["a4"].clone()
     model.fuse_pairs = False
@@ -448,21 +456,24 @@ def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
     assert torch.equal(out_p, out_l)
 
 
+@pytest.mark.parametrize("block", BLOCKS, ids=["conv3456", "pairs"])
 @pytest.mark.parametrize("per_channel", [False, True])
-def test_conv_pairs_equal_layerwise(dev, per_channel):
-    """conv3+conv4 and conv5+conv6 as fused block launches (middle activation
-    in LDS only) give the per-layer kernels' outputs bit for bit — the
-    conv4 output, the chunk-major conv6 output and the logits — and the
-    per-layer path itself matches the golden fixture (test_full_net_*)."""
+def test_conv_pairs_equal_layerwise(dev, per_channel, block, monkeypatch):
+    """conv3..conv6 as one launch, and conv3+conv4 / conv5+conv6 as two pair
+    launches (middle activations in LDS only), give the per-layer kernels'
+    outputs bit for bit — the conv4 output, the chunk-major conv6 output and
+    the logits — and the per-layer path itself matches the golden fixture
+    (test_full_net_*)."""
     import netfix
     from qconvnet import ops
     from qconvnet.qmodel import QuantizedConvNet
+    monkeypatch.setenv("QCN_CONV3456", block[0])
     z = netfix.load(per_channel)
     spec, _ = netfix.static_spec(z)
     x = torch.from_numpy(netfix.images(z)).to(dev)
     n = x.shape[0]
     model = QuantizedConvNet(spec, dev)
-    assert "conv34" in model.kernel_names(x.shape)
+    assert block[1] in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     b = model.buffers(n)
     a4_p = b["a4"].clone()
@@ -478,25 +489,39 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     assert np.array_equal(out_p.cpu().numpy(), z["logits"])
 
 
+@pytest.mark.parametrize("impl", ["conv3456", "ga", "ring"])
 @pytest.mark.parametrize("n", [1, 6, 300, 1023, 1028])
-def test_conv56_pair_workgroup_shapes_equal_layerwise(dev, n):
-    """conv5+conv6 pair at batch sizes around its two tilings: fewer than four
-    images per CU takes two images per 4-wave workgroup (1, 6, 300, 1023,
-    the last workgroup holding one image when n is odd); from 1024 on four
-    images per 8-wave workgroup (1028: a ragged last workgroup).  conv6's
-    output and the logits equal the per-layer kernels' bit for bit."""
+def test_conv56_pair_workgroup_shapes_equal_layerwise(dev, n, impl, monkeypatch):
+    """conv5+conv6 at batch sizes around the tilings: two images per 4-wave
+    workgroup (conv3456 and the weights-from-L2 pair "ga"; the last
+    workgroup holds one image when n is odd) and the LDS-ring pair ("ring":
+    two images per 4-wave workgroup below four images per CU, four per 8-wave
+    workgroup from 1024 on, 1028 a ragged last workgroup).  conv4's and
+    conv6's outputs and the logits equal the per-layer kernels' bit for bit."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
     from oracle import torch_ref
+    monkeypatch.setenv("QCN_CONV3456", "1" if impl == "conv3456" else "0")
+    # QCN_PAIR56 is read once per process by the library: the ring case runs
+    # only when this process chose it
+    if impl == "ring" and os.environ.get("QCN_PAIR56", "4") != "0":
+        pytest.skip("the LDS-ring conv5+6 pair runs with QCN_PAIR56=0 set before the library loads")
+    if impl == "ga" and os.environ.get("QCN_PAIR56", "4") == "0":
+        pytest.skip("QCN_PAIR56=0 in this process")
     spec, _ = netfix.static_spec(netfix.load(False))
     x = torch.from_numpy(torch_ref.synthetic_images(n, 13)).to(dev)
     model = QuantizedConvNet(spec, dev)
-    assert model.kernel_names(x.shape)[2] == "conv56"
+    assert model.kernel_names(x.shape)[1:3] == (("conv3456", "fc12" if n % 128 == 0 else "fc1")
+                                                if impl == "conv3456" else ("conv34", "conv56"))
     out_p = model.run(x).clone()
+    a4_p = model.buffers(n)["a4"].clone()
     a6_p = model.buffers(n)["a6"].clone()
     model.fuse_pairs = False
     out_l = model.run(x).clone()
+    a4_l = model.buffers(n)["a4"]
     a6_l = model.buffers(n)["a6"]
     torch.cuda.synchronize()
-    assert torch.equal(a6_p, a6_l)
+    assert torch.equal(a4_p, a4_l)
+    if n % 128:   # (n % 128 == 0 writes conv6 chunk-major for the head: checked via the logits)
+        assert torch.equal(a6_p, a6_l)
     assert torch.equal(out_p, out_l)
