@@ -50,6 +50,17 @@ void convpair_stamped(int kind, const uint8_t* __restrict__ x, int nimg, int x_z
   clk_store(kind, t0, r0);
 }
 
+template <class CA, class CB, int D>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_ga_stamped(int kind, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                         const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                         const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  convpair_ga_body<CA, CB, D>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  clk_store(kind, t0, r0);
+}
+
 __global__ __launch_bounds__(512, 1)
 void conv12p_stamped(const float* __restrict__ x, int nimg, float in_inv, int in_zp,
                      const int8_t* __restrict__ w1, ConvEpi ep1, int x2_zp,
@@ -70,6 +81,20 @@ int launch_pair_stamped(int kind, const uint8_t* x, int nimg, int x_zp, const in
   const long pix = (long)nimg * CA::IMG;
   const int grid = (int)((pix + CA::PXB - 1) / CA::PXB);
   auto k = convpair_stamped<CA, CB>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, kind, x, nimg, x_zp, wa, epa, xb_zp,
+                     wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+template <class CA, class CB, int D>
+int launch_pair_ga_stamped(int kind, const uint8_t* x, int nimg, int x_zp, const int8_t* wa,
+                           const ConvEpi& epa, int xb_zp, const int8_t* wb, const ConvEpi& epb,
+                           uint8_t* y, hipStream_t st) {
+  using P = PairGaCfg<CA, CB>;
+  const long pix = (long)nimg * CA::IMG;
+  const int grid = (int)((pix + CA::PXB - 1) / CA::PXB);
+  auto k = convpair_ga_stamped<CA, CB, D>;
   static bool attr_done[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
   hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, kind, x, nimg, x_zp, wa, epa, xb_zp,
@@ -106,16 +131,10 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     return launch_pair_stamped<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                                ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
-    const int ncu = qcn_cu_count();
-    if (ncu > 0 && nimg < 4 * ncu)
-      return launch_pair_stamped<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
-                                 ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>>(
-          2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    return launch_pair_stamped<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
-                               ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
+  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256)   // the product's default form
+    return launch_pair_ga_stamped<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
+                                  ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>, 4>(
         2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-  }
   return QCN_ERR_UNSUPPORTED;
 }
 

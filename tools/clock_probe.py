@@ -42,7 +42,7 @@ def grid_of(name, n, ncu):
         return min(n, ncu)
     if name == "conv34":
         return n                       # one 16x16 image (256 pixels) per 4-wave workgroup
-    return (n * 64 + 127) // 128 if n < 4 * ncu else (n * 64 + 255) // 256
+    return (n + 1) // 2                # two 8x8 images per 4-wave workgroup (convpair_ga_kernel)
 
 
 def main():
