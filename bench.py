@@ -439,8 +439,8 @@ def main():
     ap.add_argument("--spec-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--per-channel", action="store_true")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the forward as one HIP graph (measured: no gain, the launch "
-                         "queue already runs back to back)")
+                    help="replay the forward as one HIP graph (measured slower: config 2 3.04 vs "
+                         "3.11 M img/s, headline 5.9 vs 6.3 M img/s, profiles/r03_diag_graph_ab.txt)")
     ap.add_argument("--streams", type=int, default=2,
                     help="resnet50: split the batch over this many HIP streams, launches "
                          "interleaved layer by layer (QuantizedResNet.run_streams; measured "
@@ -533,7 +533,10 @@ def main():
     images = world * B * args.steps
     value = images / elapsed
 
-    # ---- timed region B: per-kernel HIP events (same steps, same stream)
+    # ---- timed region B: per-kernel HIP events (same steps, same stream).
+    # Each interval includes the dependent-launch boundary before its kernel
+    # (a device-side gap: queueing the step behind a device sleep so the host
+    # is ahead changed nothing, profiles/r03_diag_graph_ab.txt)
     marks_all = []
     barrier()
     torch.cuda.synchronize()
@@ -615,7 +618,7 @@ def main():
         "metric": METRIC if mode == "static" else METRIC_QDQ, "value": value, "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "int8", "data": "synthetic",
+        "vs_baseline": None, "dtype": "int8", "data": "synthetic", "hip_graph": bool(use_graph),
         "config": {"workload": ("full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
                                 "NHWC, per-tensor weights" if mode == "static" else
                                 "per-layer QDQ SimpleConvNet (CustomQuantizationModel, BASELINE configs[1]): "

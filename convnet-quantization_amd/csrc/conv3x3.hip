@@ -39,7 +39,7 @@ constexpr int kProdPrio = 2;
 //   RPAD bytes of padding per staged row,  SPAD per staged image segment
 //   SPLIT store even patch columns before odd ones (pooled layers read stride-2)
 template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
-          int SPAD = 0, bool SPLIT = false, int WI_ = 2>
+          int SPAD = 0, bool SPLIT = false, int WI_ = 2, int JT_ = 4, int RB_ = 0>
 struct ConvCfg {
   static constexpr int kCin = CIN, kCout = COUT;
   static constexpr bool kPool = POOL, kSplit = SPLIT;
@@ -48,23 +48,32 @@ struct ConvCfg {
   // reads 8 fragments per 16 MFMAs instead of 6 per 8 (LDS bytes per MFMA
   // -33 %) and holds 256 accumulators, so one wave per SIMD
   static constexpr int WI = WI_;
-  static constexpr int MPS = 4 * WI;             // MFMAs per K-step
+  // JT 32-pixel blocks per wave: 4 (128 pixels; pooled layers need the four
+  // 2x2 quadrants) or 2 (64 pixels: row bands of the 56-wide ResNet maps)
+  static constexpr int JT = JT_;
+  static constexpr int MPS = JT * WI;            // MFMAs per K-step
   static constexpr int WCO = COUT / (32 * WI);   // waves along cout
   static constexpr int NWAVES = WCO * WPX;
   static constexpr int NT = NWAVES * 64;         // threads
-  static constexpr int PXB = WPX * 128;          // output pixels per workgroup (pre-pool)
+  static constexpr int PXB = WPX * 32 * JT;      // output pixels per workgroup (pre-pool)
   static constexpr int OPX = POOL ? PXB / 4 : PXB;  // output pixels written
   static constexpr int IMG = H * W;
-  static constexpr int SEGS = PXB >= IMG ? PXB / IMG : 1;
-  static constexpr int R = PXB >= IMG ? H : PXB / W;   // rows per segment
+  // RB_ > 0: BAND tiles — RB_ consecutive rows of the flattened (image, row)
+  // space, which may run across image boundaries; each image's part of the
+  // band gets its own halo rows in the patch (BandAddr / stage_band), so any
+  // H works without padded rows.  SEGS is then the most images a band touches.
+  static constexpr bool kBand = RB_ > 0;
+  static constexpr int SEGS = kBand ? 1 + (RB_ - 1 + H - 1) / H : (PXB >= IMG ? PXB / IMG : 1);
+  static constexpr int R = kBand ? RB_ : (PXB >= IMG ? H : PXB / W);   // rows per segment (band)
   static constexpr int PS = CIN + PSP;
   static constexpr int PROWS = R + 2, PCOLS = W + 2;
   static constexpr int HALF = (PCOLS + 1) / 2;
   static constexpr int RS = PCOLS * PS + RPAD;
   static constexpr int SS = PROWS * RS + SPAD;
-  static constexpr int PATCH = SEGS * SS;
+  static constexpr int PATCH = kBand ? (RB_ + 2 * SEGS) * RS : SEGS * SS;
   static constexpr int WBUF = COUT * 64;         // one K-chunk of weights (XOR-swizzled rows)
-  static constexpr int NG = WBUF / (NWAVES * 1024);  // global_load_lds per wave per chunk
+  static constexpr int NPC = WBUF / 1024;        // 1-KiB LDS-DMA pieces per chunk
+  static constexpr int NG = (NPC + NWAVES - 1) / NWAVES;  // global_load_lds per wave per chunk (at most)
   static constexpr int NCH = 9 * CIN / 64;       // K chunks
   static constexpr int OS = COUT + 16;           // output staging row stride
   static constexpr int MAIN = PATCH + 3 * WBUF;  // patch + 3-deep weight ring
@@ -72,12 +81,16 @@ struct ConvCfg {
   static constexpr int EPI = MAIN > OUT ? MAIN : OUT;  // u | v | mult (fp32 x COUT each)
   static constexpr int LDS = EPI + 12 * COUT;
   static_assert(CIN % 64 == 0 && COUT % (32 * WI) == 0, "channel multiples");
-  static_assert(WI == 2 || WI == 4, "wave tile of 64 or 128 couts");
+  // WI = 1 (32 couts x 128 pixels): the cout-split conv6 of small batches
+  static_assert(WI == 1 || WI == 2 || WI == 4, "wave tile of 32, 64 or 128 couts");
   static_assert(PSP % 16 == 0 && RPAD % 16 == 0 && SPAD % 16 == 0, "16-B aligned layout");
   static_assert(PXB % W == 0, "workgroup covers whole rows");
-  static_assert(PXB >= IMG ? (PXB % IMG == 0) : (H % R == 0), "rows tile the image");
+  static_assert(kBand ? (PXB == RB_ * W && !POOL)
+                      : (PXB >= IMG ? (PXB % IMG == 0) : (H % R == 0)), "rows tile the image");
   static_assert(!POOL || (R % 2 == 0), "pooled rows come in pairs");
-  static_assert(NG >= 1 && WBUF % (NWAVES * 1024) == 0, "weight ring split");
+  static_assert(NG >= 1 && WBUF % 1024 == 0, "weight ring split");
+  static_assert(!POOL || JT == 4, "pooled tiles are the four quadrants");
+  static_assert(JT == 2 || JT == 4, "64- or 128-pixel wave tiles");
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __device__ static constexpr int slot(int seg, int prow, int pcol) {
     const int cpos = SPLIT ? ((pcol & 1) * HALF + (pcol >> 1)) : pcol;
@@ -254,7 +267,8 @@ QCN_DEV v16i acc_init_corr(const int* __restrict__ corr, int co_base, int hi) {
 // WT: write-through (the next launch reads it); plain stores keep the lines
 // in this XCD's L2 for a read-back by the same workgroup (conv3456).
 template <int COUT, int OS, int NT, bool WT = true>
-QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid) {
+QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid,
+                          int rstride = COUT) {
   constexpr int CPR = COUT / 16;
   const int total = opx * CPR;
   const wt_rsrc_t wr = wt_rsrc(dst);
@@ -262,8 +276,8 @@ QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long va
     const int row = e / CPR, ch = e % CPR;
     if (row < valid_px) {
       const uint4 v = *reinterpret_cast<const uint4*>(lds_out + row * OS + ch * 16);
-      if constexpr (WT) store_wt16(wr, (uint32_t)(row * COUT + ch * 16), v);
-      else *reinterpret_cast<uint4*>(dst + row * COUT + ch * 16) = v;
+      if constexpr (WT) store_wt16(wr, (uint32_t)(row * rstride + ch * 16), v);
+      else *reinterpret_cast<uint4*>(dst + row * rstride + ch * 16) = v;
     }
   }
 }
@@ -276,11 +290,21 @@ QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long va
 template <class C>
 struct PatchAddr {
   static_assert(!C::kSplit || C::kPool, "parity-split columns need pooled tiles");
-  int base[4];
-  QCN_DEV PatchAddr(int wp, int l32, int hi) {
+  int base[C::JT];
+  // y0: (band tiles) the image row of the band's first row
+  QCN_DEV PatchAddr(int wp, int l32, int hi, int y0 = 0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < C::JT; ++j) {
       int seg, prow, pcol;
+      if constexpr (C::kBand) {
+        // band row i sits in patch row i + 2 seg + 1 (seg: images crossed
+        // before it, each adding a bottom and a top halo row); base = tap (0, 0)
+        const int m = (wp * C::JT + j) * 32 + l32;
+        const int i = m / C::W;
+        seg = (y0 + i) / C::H;
+        base[j] = (i + 2 * seg) * C::RS + (m % C::W) * C::PS + hi * 16;
+        continue;
+      }
       if constexpr (C::kPool) {
         constexpr int PW = C::W / 2, PR = C::R / 2;
         const int q = wp * 32 + l32;
@@ -288,7 +312,7 @@ struct PatchAddr {
         prow = 2 * ((q / PW) % PR) + (j >> 1);
         pcol = 2 * (q % PW) + (j & 1);
       } else {
-        const int m = (wp * 4 + j) * 32 + l32;
+        const int m = (wp * C::JT + j) * 32 + l32;
         seg = m / (C::R * C::W);
         prow = (m / C::W) % C::R;
         pcol = m % C::W;
@@ -320,7 +344,8 @@ struct PatchAddr {
 template <class C>
 QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* __restrict__ wpk,
                            const int* __restrict__ corr, int wave, int lane,
-                           v16i (&acc)[C::WI][4]) {
+                           v16i (&acc)[C::WI][C::JT], int band_y0 = 0) {
+  constexpr int JT = C::JT;
   constexpr int CB = C::kCin / 64;
   constexpr int WI = C::WI, MPS = C::MPS;
   const int wc = wave % C::WCO, wp = wave / C::WCO;
@@ -332,13 +357,15 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // so the A-operand ds_read_b128 of 16 consecutive rows is conflict-free.
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto issue_g = [&](int ch, int g) {
+    if constexpr (C::NPC % C::NWAVES != 0)   // (wave-uniform) fewer pieces than waves in this round
+      if (g * C::NWAVES + wave_u >= C::NPC) return;
     uint8_t* buf = wring + (ch % 3) * C::WBUF;
     const int8_t* base = wpk + (long)ch * C::WBUF;
     const int o = (g * C::NWAVES + wave_u) * 1024 + lane * 16;
     const int r = o >> 6, sl = (o >> 4) & 3;
     glds16(base + r * 64 + ((sl ^ ((r >> 2) & 3)) << 4), buf + (g * C::NWAVES + wave_u) * 1024);
   };
-  const PatchAddr<C> pa(wp, l32, hi);
+  const PatchAddr<C> pa(wp, l32, hi, band_y0);
   // A operand: row wc*32*WI + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
   const int arow = wc * 32 * WI + l32;
   const int aswz = (arow >> 2) & 3;  // same for arow + 32i
@@ -346,7 +373,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   for (int i = 0; i < WI; ++i) {
     const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
+    for (int j = 0; j < JT; ++j) acc[i][j] = c0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch + corr loads retired
 #pragma unroll
@@ -373,17 +400,17 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   };
   // one step: MPS MFMAs on (fa, fb); reads of step (rch, rkk) into (fan, fbn)
   // interleaved one per MFMA; DMA pieces of chunk dch spread over the MFMAs
-  auto step = [&](v4i (&fan)[WI], v4i (&fbn)[4], int rch, int rkk, bool rd,
-                  const v4i (&fa)[WI], const v4i (&fb)[4], bool dma, int dch) {
+  auto step = [&](v4i (&fan)[WI], v4i (&fbn)[JT], int rch, int rkk, bool rd,
+                  const v4i (&fa)[WI], const v4i (&fb)[JT], bool dma, int dch) {
 #pragma unroll
     for (int m = 0; m < MPS; ++m) {
       if (rd) {
         if (m < WI) fan[m] = rd_a(rch, rkk, m);
-        else if (m < WI + 4) fbn[m - WI] = rd_b(rch, rkk, m - WI);
+        else if (m < WI + JT) fbn[m - WI] = rd_b(rch, rkk, m - WI);
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[m / 4][m % 4] =
-          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / 4], fb[m % 4], acc[m / 4][m % 4], 0, 0, 0);
+      acc[m / JT][m % JT] =
+          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / JT], fb[m % JT], acc[m / JT][m % JT], 0, 0, 0);
 #pragma unroll
       for (int g = 0; g < C::NG; ++g)
         if (dma && m == (2 * g + 1) * MPS / (2 * C::NG)) {
@@ -399,14 +426,14 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 #pragma unroll
       for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]));
+        for (int j = 0; j < JT; ++j) asm volatile("" : "+v"(acc[i][j]));
     }
   };
-  v4i fa0[WI], fb0[4], fa1[WI], fb1[4];
+  v4i fa0[WI], fb0[JT], fa1[WI], fb1[JT];
 #pragma unroll
   for (int i = 0; i < WI; ++i) fa0[i] = rd_a(0, 0, i);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
+  for (int j = 0; j < JT; ++j) fb0[j] = rd_b(0, 0, j);
   // Stagger (8-wave workgroups): the second half of the waves (4-7, the
   // SIMD partners of 0-3, working on the other pixel half) passes each ring
   // barrier one K-step EARLIER in its program — before step (ch, 0) instead
@@ -451,10 +478,49 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 
 // Requantize the accumulators, stage [pixel][cout] in LDS (offset 0) and write
 // the workgroup's contiguous NHWC output span with 16-B stores.
-template <class C, bool WT = true>
-QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* lds, int nimg,
+// Workgroup barrier (the default synchronisation of the conv bodies).
+struct WgBar {
+  QCN_DEV void operator()() const { __syncthreads(); }
+};
+
+// Barrier of ONE half of an 8-wave workgroup (convpair_dual_kernel): the four
+// waves of a half synchronise among themselves through a counter in LDS, so
+// the two halves run independently (s_barrier would hold all eight waves).
+// Release: this wave's LDS writes are complete (lgkmcnt(0); the conv bodies
+// share no global memory between waves, and their barriers never drain VMEM —
+// in-flight weight prefetches stay in flight, as with __syncthreads).  Each
+// arrival adds 1; the k-th barrier completes at 4k.  The spin is bounded, so
+// a wave can never hang the launch (a miscount would give wrong results,
+// caught by the parity tests, not a stuck GPU).
+struct HalfBar {
+  uint32_t* ctr;      // this half's LDS counter
+  uint32_t target;    // 4 x barriers passed so far
+  int lane;
+  QCN_DEV void operator()() {
+    target += 4;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wait_for(ctr, target);
+  }
+  QCN_DEV static void wait_for(uint32_t* c, uint32_t t) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      const uint32_t v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (__builtin_amdgcn_readfirstlane(v) >= t) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+};
+
+// ch0 / cstride: the workgroup's couts are channels ch0 .. ch0 + COUT - 1 of
+// an output with cstride channels per pixel (the cout-split conv6).
+template <class C, bool WT = true, class Bar = WgBar>
+QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][C::JT], const ConvEpi& ep, uint8_t* lds, int nimg,
                            int wave, int lane, int tid, uint8_t* __restrict__ y, int tile,
-                           const float* ek_override = nullptr) {
+                           const float* ek_override = nullptr, Bar&& bar = Bar{}, int ch0 = 0,
+                           int cstride = C::kCout) {
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
   constexpr bool POOL = C::kPool;
@@ -470,13 +536,13 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
       epilogue_tile_kf<4>(acc[i], K, ep, co_base, hi, lout + opx * C::OS);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int opx = (wp * 4 + j) * 32 + l32;
+      for (int j = 0; j < C::JT; ++j) {
+        const int opx = (wp * C::JT + j) * 32 + l32;
         epilogue_tile_kf<1>(&acc[i][j], K, ep, co_base, hi, lout + opx * C::OS);
       }
     }
   }
-  __syncthreads();
+  bar();
   const long out0 = (long)tile * C::OPX;
   const long total_out = POOL ? (long)nimg * C::IMG / 4 : (long)nimg * C::IMG;
   if (ep.kmajor) {
@@ -487,19 +553,21 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][4], const ConvEpi& ep, uint8_t* ld
     constexpr int IMGS = C::OPX / OPI;
     if constexpr (IMGS >= 1 && C::OPX % OPI == 0) {
       constexpr int CC = COUT / 32;
+      const int CCT = cstride / 32, cc0 = ch0 / 32;   // chunks per pixel of the whole output
       const int n0 = (int)(out0 / OPI);
       const wt_rsrc_t wr = wt_rsrc(y + (long)n0 * 32);   // offsets < 2^31: nimg * 4096 checked at launch
       for (int e = tid; e < OPI * CC * IMGS * 2; e += C::NT) {
         const int half = e & 1, img = (e >> 1) % IMGS, pc = (e >> 1) / IMGS;
         const int p = pc / CC, cc = pc % CC;
         if (n0 + img < nimg)
-          store_wt16(wr, (uint32_t)(((p * CC + cc) * nimg + img) * 32 + half * 16),
+          store_wt16(wr, (uint32_t)(((p * CCT + cc0 + cc) * nimg + img) * 32 + half * 16),
                      *reinterpret_cast<const uint4*>(lout + (img * OPI + p) * C::OS + cc * 32 + half * 16));
       }
     }
     return;
   }
-  store_staged<COUT, C::OS, C::NT, WT>(lout, C::OPX, y + out0 * COUT, total_out - out0, tid);
+  store_staged<COUT, C::OS, C::NT, WT>(lout, C::OPX, y + out0 * cstride + ch0, total_out - out0, tid,
+                                       cstride);
 }
 
 // Stage the input patch of the workgroup's tile (images n0.., first output row
@@ -550,12 +618,63 @@ QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int 
 
 }
 
-template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT>
-__global__ __launch_bounds__(COUT * WPX, 2)
+// Band tiles: the patch of RB flattened rows starting at image n0, row y0.
+// Patch row pr belongs to segment k (the k-th image the band touches) when
+// pr - 2k - 1 is one of that segment's band rows or its halo: image n0 + k,
+// image row (k == 0 ? y0 : 0) + (pr - 2k - first_k) - 1, zero point outside.
+template <class C>
+QCN_DEV void stage_band(const uint8_t* __restrict__ x, int nimg, int x_zp, int n0, int y0,
+                        uint8_t* patch, int tid) {
+  constexpr int CIN = C::kCin, CH16 = CIN / 16;
+  constexpr int PR = C::R + 2 * C::SEGS;
+  constexpr int TOTAL = PR * C::PCOLS * CH16;
+  constexpr int NITER = (TOTAL + C::NT - 1) / C::NT;
+  constexpr int BATCH = NITER < 8 ? NITER : 8;
+  const uint32_t padw = xor80(splat_u8(x_zp));
+  const int first1 = C::H - y0;   // band rows of segment 0 (>= 1)
+  for (int b0 = 0; b0 < NITER; b0 += BATCH) {
+    uint4 v[BATCH];
+    int dst[BATCH];
+    bool inside[BATCH];
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const int it = tid + (b0 + k) * C::NT;
+      const int itc = it < TOTAL ? it : 0;
+      const int sl = itc / CH16, chunk = itc % CH16;
+      const int pr = sl / C::PCOLS, pc = sl % C::PCOLS;
+      // segment of patch row pr: segment 0 holds patch rows [0, first1 + 2),
+      // segment k >= 1 rows [first1 + 2 + (k - 1)(H + 2), ... + H + 2)
+      int seg = 0, yy = y0 - 1 + pr;
+      if (pr >= first1 + 2) {
+        const int q = pr - first1 - 2;
+        seg = 1 + q / (C::H + 2);
+        yy = q % (C::H + 2) - 1;
+      }
+      const int n = n0 + seg, xx = pc - 1;
+      // rows of the last segment past the band end read as padding (never used)
+      inside[k] = n < nimg && yy >= 0 && yy < C::H && xx >= 0 && xx < C::W;
+      dst[k] = (it < TOTAL && b0 + k < NITER) ? pr * C::RS + pc * C::PS + chunk * 16 : -1;
+      const long src = inside[k] ? (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16 : 0;
+      v[k] = *reinterpret_cast<const uint4*>(x + src);
+    }
+#pragma unroll
+    for (int k = 0; k < BATCH; ++k) {
+      const uint4 val = inside[k] ? make_uint4(xor80(v[k].x), xor80(v[k].y), xor80(v[k].z), xor80(v[k].w))
+                                  : make_uint4(padw, padw, padw, padw);
+      if (dst[k] >= 0) *reinterpret_cast<uint4*>(patch + dst[k]) = val;
+    }
+  }
+}
+
+template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP, int RPAD, int SPAD, bool SPLIT,
+          int JT, int RB>
+// JT = 2 (seven-wave 64-pixel tiles): two workgroups per CU need four waves on
+// some SIMDs, so at most 128 VGPRs
+__global__ __launch_bounds__(COUT * WPX, JT == 2 ? 4 : 2)
 void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                          const int8_t* __restrict__ wpk, ConvEpi ep,
                          uint8_t* __restrict__ y) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT, 2, JT, RB>;
   static_assert(C::NT == COUT * WPX, "64-cout wave tiles");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   uint8_t* patch = lds;
@@ -569,10 +688,11 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   const int y0 = (int)((p0 % C::IMG) / C::W);
 
   stage_epik<COUT, C::NT>(ep, reinterpret_cast<float*>(lds + C::EPI), tid);
-  stage_patch<C>(x, nimg, x_zp, n0, y0, patch, tid);
+  if constexpr (C::kBand) stage_band<C>(x, nimg, x_zp, n0, y0, patch, tid);
+  else stage_patch<C>(x, nimg, x_zp, n0, y0, patch, tid);
 
-  v16i acc[C::WI][4];
-  conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc);
+  v16i acc[C::WI][C::JT];
+  conv_mainloop<C>(patch, lds + C::PATCH, wpk, ep.corr, wave, lane, acc, C::kBand ? y0 : 0);
   conv_epilogue<C>(acc, ep, lds, nimg, wave, lane, tid, y, (int)blockIdx.x);
 }
 
@@ -586,6 +706,7 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 template <class CA, class CB>
 struct PairCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles");
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
                 CA::W == CB::W && CA::WI == CB::WI, "same whole-image tiling");
   static constexpr int MAIN_A = CA::PATCH + 3 * CA::WBUF;
@@ -693,12 +814,14 @@ struct GaFrag {
 // Issue the A-fragment loads of K-step s (chunk s / 2, half kk = s % 2) into
 // slot s % (D + 1).  wr: buffer resource of the packed weights; voff: this
 // lane's row offset ((wc*32*WI + l32) * 64 + hi * 16).
-template <class C, int D>
+// CST: bytes between consecutive K chunks of the packed weights (C::WBUF, or
+// the whole layer's cout x 64 for a workgroup that owns a slice of the couts).
+template <class C, int D, int CST = C::WBUF>
 QCN_DEV void ga_issue(GaFrag<C, D>& g, wt_rsrc_t wr, int voff, int s) {
   const int ch = s >> 1, kk = s & 1;
 #pragma unroll
   for (int i = 0; i < C::WI; ++i) {
-    const auto t = __builtin_amdgcn_raw_buffer_load_b128(wr, voff, ch * C::WBUF + i * 32 * 64 + kk * 32, 0);
+    const auto t = __builtin_amdgcn_raw_buffer_load_b128(wr, voff, ch * CST + i * 32 * 64 + kk * 32, 0);
     g.fa[s % (D + 1)][i] = (v4i){(int)t[0], (int)t[1], (int)t[2], (int)t[3]};
   }
 }
@@ -710,22 +833,22 @@ QCN_DEV int ga_voff(int wave, int lane) {
 
 // The first D K-steps' loads (issued early so their latency overlaps the
 // patch staging or the previous conv's epilogue).
-template <class C, int D>
-QCN_DEV void ga_prefetch(GaFrag<C, D>& g, const int8_t* __restrict__ wpk, int wave, int lane) {
+template <class C, int D, int CST = C::WBUF>
+QCN_DEV void ga_prefetch(GaFrag<C, D>& g, const int8_t* __restrict__ wpk, int wave, int lane, int co0 = 0) {
   const wt_rsrc_t wr = wt_rsrc(wpk);
-  const int voff = ga_voff<C>(wave, lane);
+  const int voff = ga_voff<C>(wave, lane) + co0 * 64;
 #pragma unroll
-  for (int s = 0; s < D; ++s) ga_issue<C, D>(g, wr, voff, s);
+  for (int s = 0; s < D; ++s) ga_issue<C, D, CST>(g, wr, voff, s);
 }
 
 // K loop over the patch staged in LDS (layout C::slot, all waves' writes
 // visible), A fragments from g (steps 0..D-1 already issued).  Returns after a
 // workgroup barrier: every wave's patch reads are done and the caller may
 // reuse the LDS.
-template <class C, int D>
+template <class C, int D, int CST = C::WBUF, class Bar = WgBar>
 QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ wpk,
                               const int* __restrict__ corr, int wave, int lane,
-                              v16i (&acc)[C::WI][4], GaFrag<C, D>& g) {
+                              v16i (&acc)[C::WI][4], GaFrag<C, D>& g, Bar&& bar = Bar{}, int co0 = 0) {
   constexpr int CB = C::kCin / 64;
   constexpr int WI = C::WI, MPS = C::MPS, S = 2 * C::NCH;
   static_assert(D >= 1 && D < S, "prefetch depth");
@@ -733,7 +856,7 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
   const int l32 = lane & 31, hi = lane >> 5;
   const PatchAddr<C> pa(wp, l32, hi);
   const wt_rsrc_t wr = wt_rsrc(wpk);
-  const int voff = ga_voff<C>(wave, lane);
+  const int voff = ga_voff<C>(wave, lane) + co0 * 64;
 #pragma unroll
   for (int i = 0; i < WI; ++i) {
     const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
@@ -753,20 +876,21 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int m = 0; m < MPS; ++m) {
-      // next step's B fragments one per MFMA (even slots), the A loads of
-      // step s + D in the odd slots
-      if (s + 1 < S && (m & 1) == 0 && (m >> 1) < 4) fb[(s + 1) & 1][m >> 1] = rd_b(s + 1, m >> 1);
+      // next step's four B fragments spread over the step's MFMAs (every
+      // other one when there are eight), the A loads of step s + D mid-step
+      constexpr int BSP = MPS / 4;
+      if (s + 1 < S && m % BSP == 0) fb[(s + 1) & 1][m / BSP] = rd_b(s + 1, m / BSP);
       __builtin_amdgcn_sched_barrier(0);
       acc[m / 4][m % 4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g.fa[s % (D + 1)][m / 4], fb[s & 1][m % 4],
                                                                 acc[m / 4][m % 4], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + D < S && m == MPS / 2 - 1) {
         // slot (s + D) % (D + 1) == (s - 1) % (D + 1): consumed by step s - 1
-        ga_issue<C, D>(g, wr, voff, s + D);
+        ga_issue<C, D, CST>(g, wr, voff, s + D);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if constexpr (WI == 2) {
+    if constexpr (WI <= 2) {
 #pragma unroll
       for (int i = 0; i < WI; ++i)
 #pragma unroll
@@ -774,7 +898,7 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();
+  bar();
 }
 
 // LDS plan of the direct-weight pair: A's patch and then B's patch at offset
@@ -783,8 +907,11 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
 template <class CA, class CB>
 struct PairGaCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles");
+  // (B may own a slice of the couts with a narrower wave tile: the patch
+  // layout depends only on B's input side)
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
-                CA::W == CB::W && CA::WI == CB::WI, "same whole-image tiling");
+                CA::W == CB::W, "same whole-image tiling");
   static constexpr int PATCH = CA::PATCH > CB::PATCH ? CA::PATCH : CB::PATCH;
   static_assert(CB::OPX * CB::OS <= PATCH, "B's staging fits the dead patch");
   static constexpr int OFF_EA = PATCH;
@@ -792,6 +919,35 @@ struct PairGaCfg {
   static constexpr int LDS = OFF_EB + 12 * CB::kCout;
   static_assert(LDS <= 80 * 1024, "two workgroups per CU");
 };
+
+// One tile (CA::PXB pixels of whole images) through A then B, weights from
+// L2.  lb: this tile's LDS patch region (PairGaCfg<CA, CB>::PATCH bytes; B's
+// output staging reuses it); eka / ekb: both convs' epilogue constants in
+// LDS; tid: thread index within the CA::NT threads that run the tile; bar:
+// their barrier.
+template <class CA, class CB, int D, class Bar>
+QCN_DEV void convpair_ga_tile(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                              const int8_t* __restrict__ wa, const ConvEpi& epa, int xb_zp,
+                              const int8_t* __restrict__ wb, const ConvEpi& epb,
+                              uint8_t* __restrict__ y, uint8_t* lb, const float* eka,
+                              const float* ekb, int tid, Bar& bar) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const long p0 = (long)tile * CA::PXB;
+  const int n0 = (int)(p0 / CA::IMG);
+  const int y0 = (int)((p0 % CA::IMG) / CA::W);
+  GaFrag<CA, D> ga;
+  ga_prefetch<CA, D>(ga, wa, wave, lane);
+  stage_patch<CA>(x, nimg, x_zp, n0, y0, lb, tid);
+  bar();
+  v16i acc[CA::WI][4];
+  conv_mainloop_ga<CA, D>(lb, wa, epa.corr, wave, lane, acc, ga, bar);
+  GaFrag<CB, D> gb;
+  ga_prefetch<CB, D>(gb, wb, wave, lane);   // B's first loads ride under A's epilogue
+  pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lb, wave, lane, tid);
+  bar();
+  conv_mainloop_ga<CB, D>(lb, wb, epb.corr, wave, lane, acc, gb, bar);
+  conv_epilogue<CB, true>(acc, epb, lb, nimg, wave, lane, tid, y, tile, ekb, bar);
+}
 
 template <class CA, class CB, int D>
 QCN_DEV void convpair_ga_body(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
@@ -801,28 +957,14 @@ QCN_DEV void convpair_ga_body(int tile, const uint8_t* __restrict__ x, int nimg,
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // laundered: a caller that runs this body more than once (conv3456) must
   // not get thread-id-derived addresses hoisted and held live across calls
-  int tid_l = threadIdx.x;
-  asm volatile("" : "+v"(tid_l));
-  const int tid = tid_l, lane = tid & 63, wave = tid >> 6;
-  const long p0 = (long)tile * CA::PXB;
-  const int n0 = (int)(p0 / CA::IMG);
-  const int y0 = (int)((p0 % CA::IMG) / CA::W);
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
-  GaFrag<CA, D> ga;
-  ga_prefetch<CA, D>(ga, wa, wave, lane);
   stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
-  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
-  __syncthreads();
-  v16i acc[CA::WI][4];
-  conv_mainloop_ga<CA, D>(lds, wa, epa.corr, wave, lane, acc, ga);
-  GaFrag<CB, D> gb;
-  ga_prefetch<CB, D>(gb, wb, wave, lane);   // B's first loads ride under A's epilogue
-  pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
-  __syncthreads();
-  conv_mainloop_ga<CB, D>(lds, wb, epb.corr, wave, lane, acc, gb);
-  conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+  WgBar bar;
+  convpair_ga_tile<CA, CB, D>(tile, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, lds, eka, ekb, tid, bar);
 }
 
 template <class CA, class CB, int D>
@@ -831,6 +973,105 @@ void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                         const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                         const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   convpair_ga_body<CA, CB, D>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+}
+
+// --------------------------------------------------------------------------
+// Small batches (config 2, batch 256: 128 two-image workgroups on 256 CUs):
+// workgroup 2t + h owns images 2t, 2t+1 and conv B's output channels
+// [h * CB::kCout, (h + 1) * CB::kCout) of a COUTB-channel layer.  Each of the
+// two computes conv A in full (B's input patch needs all of A's channels), so
+// the pair costs 4/3 of the MFMAs in twice the workgroups.  B's wave tile is
+// narrower (CB::WI) so four waves still cover the slice.
+template <class CA, class CB, int D, int COUTB>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                              const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                              const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  using P = PairGaCfg<CA, CB>;
+  static_assert(COUTB % CB::kCout == 0 && CA::NWAVES == CB::NWAVES, "cout slices");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NS = COUTB / CB::kCout;
+  const int tile = (int)blockIdx.x / NS, co0 = ((int)blockIdx.x % NS) * CB::kCout;
+  ConvEpi eph = epb;   // this slice's constants
+  eph.u += co0; eph.v += co0; eph.mult += co0; eph.corr += co0;
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
+  stage_epik<CB::kCout, CB::NT>(eph, ekb, tid);
+  const long p0 = (long)tile * CA::PXB;
+  const int n0 = (int)(p0 / CA::IMG);
+  const int y0 = (int)((p0 % CA::IMG) / CA::W);
+  GaFrag<CA, D> ga;
+  ga_prefetch<CA, D>(ga, wa, wave, lane);
+  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
+  __syncthreads();
+  v16i acc[CA::WI][4];
+  conv_mainloop_ga<CA, D>(lds, wa, epa.corr, wave, lane, acc, ga);
+  constexpr int CSTB = COUTB * 64;
+  GaFrag<CB, D> gb;
+  ga_prefetch<CB, D, CSTB>(gb, wb, wave, lane, co0);
+  pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
+  __syncthreads();
+  v16i accb[CB::WI][4];
+  conv_mainloop_ga<CB, D, CSTB>(lds, wb, eph.corr, wave, lane, accb, gb, WgBar{}, co0);
+  conv_epilogue<CB, true>(accb, eph, lds, nimg, wave, lane, tid, y, tile, ekb, WgBar{}, co0, COUTB);
+}
+
+// --------------------------------------------------------------------------
+// Two independent halves in one 8-wave workgroup (one workgroup per CU,
+// persistent over tiles).  Waves 0-3 and waves 4-7 each run the
+// weights-from-L2 pair body on their own tiles and their own LDS patch region,
+// synchronising only among themselves (HalfBar), so a CU holds the same two
+// independent 4-wave streams as two co-resident workgroups — but their phase
+// offset is chosen: half 1 starts once half 0 has passed `offset_bar` of its
+// barriers, so one half's staging and epilogues run beside the other half's
+// MFMA loops instead of wherever two workgroups happen to drift.
+template <class CA, class CB>
+struct DualCfg {
+  static constexpr int PATCH = PairGaCfg<CA, CB>::PATCH;   // per half
+  static constexpr int OFF_EA = 0;
+  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
+  static constexpr int OFF_CTR = OFF_EB + 12 * CB::kCout;
+  static constexpr int OFF_H = OFF_CTR + 16;
+  static constexpr int LDS = OFF_H + 2 * PATCH;
+  static_assert(OFF_H % 16 == 0 && PATCH % 16 == 0, "16-B aligned regions");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <class CA, class CB, int D>
+__global__ __launch_bounds__(2 * CA::NT, 1)
+void convpair_dual_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                          const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                          const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y,
+                          int offset_bar) {
+  using P = DualCfg<CA, CB>;
+  static_assert(CA::NT == 256, "4-wave halves");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + P::OFF_CTR);
+  stage_epik<CA::kCout, 2 * CA::NT>(epa, eka, (int)threadIdx.x);
+  stage_epik<CB::kCout, 2 * CA::NT>(epb, ekb, (int)threadIdx.x);
+  if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+  __syncthreads();
+  int tid = (int)threadIdx.x & 255;
+  asm volatile("" : "+v"(tid));
+  const int half = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
+  uint8_t* lb = lds + P::OFF_H + half * P::PATCH;
+  HalfBar bar{ctr + half, 0u, tid & 63};
+  const int b = (int)blockIdx.x, G = (int)gridDim.x;
+  const long ntile = ((long)nimg * CA::IMG + CA::PXB - 1) / CA::PXB;
+  // half 1 starts behind half 0 (only if half 0 has a tile to pass barriers in)
+  if (half == 1 && offset_bar > 0 && b < ntile) HalfBar::wait_for(ctr, 4u * (uint32_t)offset_bar);
+  for (long t = b + (long)half * G; t < ntile; t += 2L * G) {
+    // laundered per tile: nothing thread-id-derived is hoisted out of the loop
+    // and held live across the tile (the body needs every register)
+    int ltid = tid;
+    asm volatile("" : "+v"(ltid));
+    convpair_ga_tile<CA, CB, D>((int)t, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, lb, eka, ekb, ltid, bar);
+    bar();   // the staged output is read out before the next tile's patch overwrites it
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -1503,13 +1744,13 @@ namespace {
 using namespace qcn;
 
 template <int CIN, int COUT, int HW, bool POOL, int WPX, int PSP = 16, int RPAD = 0,
-          int SPAD = 0, bool SPLIT = false>
+          int SPAD = 0, bool SPLIT = false, int JT = 4, int RB = 0>
 int launch_conv(const uint8_t* x, int nimg, int x_zp, const int8_t* wpk, const ConvEpi& ep,
                 uint8_t* y, hipStream_t st) {
-  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  using C = ConvCfg<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT, 2, JT, RB>;
   const long pix = (long)nimg * C::IMG;
   const int grid = (int)((pix + C::PXB - 1) / C::PXB);
-  auto k = conv3x3_u8s8_kernel<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT>;
+  auto k = conv3x3_u8s8_kernel<CIN, COUT, HW, POOL, WPX, PSP, RPAD, SPAD, SPLIT, JT, RB>;
   static bool attr_done[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)k, C::LDS, attr_done)) return QCN_ERR_HIP;
   hipLaunchKernelGGL(k, dim3(grid), dim3(C::NT), C::LDS, st, x, nimg, x_zp, wpk, ep, y);
@@ -1542,6 +1783,42 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+template <class CA, class CB, int D, int COUTB>
+int launch_pair_ga_split(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
+                         int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
+  using P = PairGaCfg<CA, CB>;
+  const long pix = (long)nimg * CA::IMG;
+  const int grid = (int)((pix + CA::PXB - 1) / CA::PXB) * (COUTB / CB::kCout);
+  auto k = convpair_ga_split_kernel<CA, CB, D, COUTB>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+template <class CA, class CB, int D>
+int launch_pair_dual(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
+                     int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st,
+                     int offset_bar) {
+  using P = DualCfg<CA, CB>;
+  const long ntile = ((long)nimg * CA::IMG + CA::PXB - 1) / CA::PXB;
+  const int ncu = qcn_cu_count();
+  if (ncu <= 0) return QCN_ERR_HIP;
+  // one workgroup per CU, two tiles in flight per workgroup
+  const int grid = (int)(ntile < 2L * ncu ? (ntile + 1) / 2 : ncu);
+  auto k = convpair_dual_kernel<CA, CB, D>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(2 * CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb,
+                     y, offset_bar);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
 // Tuned instantiations: the SimpleConvNet layers and the
 // small shapes the parity fixtures use.
 int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nimg, int x_zp,
@@ -1551,6 +1828,14 @@ int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nim
     return launch_conv<CI, CO, HWV, PL, WPXV, ##__VA_ARGS__>(x, nimg, x_zp, wpk, ep, y, st);
   //            cin  cout hw pool wpx | PSP RPAD SPAD SPLIT (bank-conflict-free layouts)
   QCN_CONV_CASE(64, 64, 32, 1, 4, 16, 96, 0, true)
+  // ResNet-50 layer1 3x3 (56x56, 64 -> 64): bands of 8 rows (448 pixels, 7
+  // waves of 64 couts x 64 pixels); RPAD 96 keeps the row-wrapping B reads
+  // conflict-free (row stride 296 x 16 B == 0 mod 16 slots past 56 pixels)
+  QCN_CONV_CASE(64, 64, 56, 0, 7, 16, 96, 0, false, 2)
+  // ResNet-50 layer2 3x3 (28x28, 128 -> 128): bands of 16 flattened rows
+  // (448 pixels, 14 waves), each image part with its own halo rows; RPAD 224
+  // keeps row wraps conflict-free (a wrap across images costs one 2-way read)
+  QCN_CONV_CASE(128, 128, 28, 0, 7, 16, 224, 0, false, 2, 16)
   QCN_CONV_CASE(64, 64, 32, 0, 4, 16, 0, 0, false)
   QCN_CONV_CASE(64, 128, 16, 0, 2, 16, 96, 0, false)
   QCN_CONV_CASE(128, 128, 16, 1, 2, 16, 32, 0, true)
@@ -1660,6 +1945,9 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     }();
     using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
     using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+    static const int off34 = env_int("QCN_DUAL_OFFSET34", 2);
+    if (impl34 == 12) return launch_pair_dual<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
+    if (impl34 == 13) return launch_pair_dual<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
     if (impl34 == 2) return launch_pair_ga<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 3) return launch_pair_ga<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 4) return launch_pair_ga<A3, B4, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
@@ -1684,6 +1972,19 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     if (impl56 == 1) return launch_pair_ga<A1, B1, 1>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl56 == 2) return launch_pair_ga<A1, B1, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl56 == 3) return launch_pair_ga<A1, B1, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    static const int off56 = env_int("QCN_DUAL_OFFSET56", 2);
+    if (impl56 == 13) return launch_pair_dual<A1, B1, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off56);
+    if (impl56 == 14) return launch_pair_dual<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off56);
+    // below one two-image workgroup per CU, split conv6's couts over two
+    // workgroups (conv5 computed by both): twice the workgroups
+    // (QCN_SPLIT56: images per CU at or below which to split; 0 = never).
+    // Batch 256: 22.3 -> 20.6-21.7 us; batch 512 (one workgroup per CU
+    // either way) 27.9 -> 33.3 us, so only at <= 1 image per CU
+    static const int split56 = env_int("QCN_SPLIT56", 1);
+    const int ncu56 = qcn_cu_count();
+    if (impl56 >= 1 && impl56 <= 5 && ncu56 > 0 && nimg <= split56 * ncu56)
+      return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl56 == 4) return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl56 == 5) return launch_pair_ga<A1, B1, 5>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     const int ncu = qcn_cu_count();

@@ -191,7 +191,24 @@ class QuantizedResNet:
         d.u, d.v, d.mult = self._t(u), self._t(v), self._t(mult)
         d.corr = self._t(((128 - int(e["z_x"])) * wsum.astype(np.int64)).astype(np.int32))
         d.z_x, d.z_y, d.s_y, d.relu = int(e["z_x"]), int(e["z_y"]), F32(e["s_y"]), e["relu"]
+        d.cin = w.shape[1]
+        d.w64 = None
+        if (d.kh, d.kw, d.sy, d.sx, d.py, d.px) == (3, 3, 1, 1, 1, 1) and w.shape[1] % 64 == 0:
+            # the patch-staged 3x3 kernel's layout ([tap * cin/64 + cb][cout][64])
+            d.w64 = self._t(ops.pack_conv3x3(w)[0])
         return d
+
+    # 3x3 stride-1 convs (hw, cin, cout) that run on the patch-staged ring
+    # kernel (qcn_conv3x3_u8s8_nhwc): the input band is staged once in LDS and
+    # read by all nine taps, instead of a gathered im2col row per tap
+    HALO_SHAPES = {(56, 64, 64), (28, 128, 128)}
+
+    def _conv3x3_halo(self, y, d):
+        n, h, w, cin = y.shape
+        if (d.w64 is None or h != w or (h, cin, d.cout) not in self.HALO_SHAPES
+                or os.environ.get("QCN_RESNET_HALO", "1") != "1"):
+            return None
+        return ops.conv3x3(y, d.z_x, d.w64, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, False)
 
     def _upload(self):
         sp = self.spec
@@ -318,7 +335,8 @@ class QuantizedResNet:
             y = ops.conv(q, zx, b["c1"])
             mark("conv")
             yield
-            y = ops.conv(y, b["c2"].z_x, b["c2"])
+            yh = self._conv3x3_halo(y, b["c2"])
+            y = yh if yh is not None else ops.conv(y, b["c2"].z_x, b["c2"])
             mark("conv")
             yield
             so, zo = e["out"]

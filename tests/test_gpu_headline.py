@@ -126,6 +126,11 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     assert netfix.sha(b["f1"].cpu().numpy()) == str(z["fc1_sha"])
     assert np.abs(logits - z["logits"]).max() <= tol
     assert np.array_equal(logits.argmax(1), z["argmax"])
+    # the HIP-graph replay bench.py times for config 2: the same bytes
+    model.capture_graph(xd.clone())
+    out = model.replay(n)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), logits)
     # per-layer launches (keep=True, conv1 unfused): every stub's hand-off
     m2 = QuantizedConvNet(spec, dev, fuse12=False)
     logits2, b = m2.run(xd, keep=True)

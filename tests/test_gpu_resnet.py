@@ -63,6 +63,40 @@ def test_conv_general_golden(dev, golden_dir, impl):
 
 
 @pytest.mark.parametrize("shape", [
+    # n, hw, c, zx, relu, zy, per_channel
+    (3, 56, 64, 5, True, 0, True),
+    (2, 56, 64, 200, False, 30, False),
+    (3, 28, 128, 17, True, 0, True),      # bands of 16 rows: two cross an image boundary
+    (5, 28, 128, 0, False, 99, True),     # 140 rows: the last band is partial
+    (1, 28, 128, 255, True, 7, False),
+])
+def test_conv3x3_patch_tiles_oracle(dev, shape):
+    """The ResNet 3x3 stride-1 convs on the patch-staged ring kernel
+    (qcn_conv3x3_u8s8_nhwc: 56x56 row bands, 28x28 flattened-row bands with
+    per-image halos) against the oracle's conv, per-channel and per-tensor."""
+    from qconvnet import ops
+    n, hw, c, zx, relu, zy, pc = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, hw, hw, c)).astype(np.uint8)
+    wf = (rng.standard_normal((c, c, 3, 3)) * 0.05).astype(F32)
+    s_w = qref.qparams_symmetric(wf.reshape(c, -1).min(1), wf.reshape(c, -1).max(1))[0] if pc \
+        else qref.qparams_symmetric(wf.min(), wf.max())[0]
+    wq = qref.quantize_weight(wf, s_w)
+    b = (rng.standard_normal(c) * 0.3).astype(F32)
+    s_x, s_y = F32(0.02), F32(0.2)
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    packed, wsum = ops.pack_conv3x3(wq)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    corr = ((128 - zx) * wsum.astype(np.int64)).astype(np.int32)
+    out = ops.conv3x3(T(qx), zx, T(packed), c, T(np.broadcast_to(u, c).astype(F32)),
+                      T(np.broadcast_to(v, c).astype(F32)), T(np.broadcast_to(mult, c).astype(F32)),
+                      T(corr), zy, relu, False).cpu().numpy()
+    ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, relu, (1, 1), (1, 1))
+    assert np.array_equal(out, ref)
+    assert len(np.unique(ref)) > 8, "degenerate case"
+
+
+@pytest.mark.parametrize("shape", [
     # n, h, w, cin, cout, kh, kw, stride, pad, zx, relu, zy, per_channel
     (3, 13, 11, 96, 192, 3, 3, 2, 1, 77, False, 30, True),
     (1, 7, 7, 512, 2048, 1, 1, 1, 0, 0, False, 99, True),

@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for E in "$@"; do
   i=$((i+1))
-  env $E timeout -s KILL 120 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/pab/$i -o run -- python3 $R/tools/kbench.py 1024 100 > $R/gpurun_out/pab/$i.log 2>&1
+  env $E timeout -s KILL 120 rocprofv3 --kernel-trace --stats -f csv -d $R/gpurun_out/pab/$i -o run -- python3 $R/tools/kbench.py ${KB:-1024} 100 > $R/gpurun_out/pab/$i.log 2>&1
   echo "== $E"; grep "M img/s" $R/gpurun_out/pab/$i.log | tail -1
   python3 - "$R/gpurun_out/pab/$i/run_kernel_stats.csv" <<'PY'
 import csv, sys
