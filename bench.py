@@ -441,6 +441,11 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay the forward as one HIP graph (measured slower: config 2 3.04 vs "
                          "3.11 M img/s, headline 5.9 vs 6.3 M img/s, profiles/r03_diag_graph_ab.txt)")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="also time the forward with this many batches in flight on as many "
+                         "HIP streams (QuantizedConvNet.run_pipelined, each batch its own buffers "
+                         "and the full forward at its own batch size): a serving-throughput "
+                         "field beside the metric, never the metric itself")
     ap.add_argument("--streams", type=int, default=2,
                     help="resnet50: split the batch over this many HIP streams, launches "
                          "interleaved layer by layer (QuantizedResNet.run_streams; measured "
@@ -532,6 +537,24 @@ def main():
         elapsed = max(a.item() for a in allt)
     images = world * B * args.steps
     value = images / elapsed
+
+    # ---- optional region C: batches in flight on several streams (serving)
+    pipelined = None
+    if args.pipeline > 1 and world == 1:
+        S = args.pipeline
+        streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
+        xs = [x] + [torch.from_numpy(data.synthetic_images(B, 200 + i)).to(dev) for i in range(S - 1)]
+        batches = [xs[k % S] for k in range(args.steps)]
+        model.run_pipelined(batches[:S], streams)   # buffers for every slot
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        model.run_pipelined(batches, streams)
+        torch.cuda.synchronize()
+        tc = time.perf_counter() - t0c
+        pipelined = {"streams": S, "value": B * args.steps / tc, "ms_per_batch": tc / args.steps * 1e3,
+                     "note": "batches of the same size in flight on S HIP streams, each with its own "
+                             "activation buffers and the whole forward; a serving-throughput figure, "
+                             "not the metric (value is one stream, one batch after another)"}
 
     # ---- timed region B: per-kernel HIP events (same steps, same stream).
     # Each interval includes the dependent-launch boundary before its kernel
@@ -630,6 +653,8 @@ def main():
         "kernels": {n: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in kern[n].items()}
                     for n in names},
     }
+    if pipelined is not None:
+        result["pipelined"] = pipelined
     if world > 1:
         result["rank_ms_per_step"] = rank_ms
         result["rank_ms_spread"] = max(rank_ms) - min(rank_ms)

@@ -405,8 +405,16 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
 #pragma unroll
     for (int m = 0; m < MPS; ++m) {
       if (rd) {
-        if (m < WI) fan[m] = rd_a(rch, rkk, m);
-        else if (m < WI + JT) fbn[m - WI] = rd_b(rch, rkk, m - WI);
+        // the WI + JT fragment reads of the next step, spread over the MPS
+        // MFMAs (read r in slot r * MPS / NR; two share a slot when NR > MPS,
+        // e.g. the 32-cout x 128-pixel tiles: 5 reads over 4 MFMAs)
+        constexpr int NR = WI + JT;
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          if (r * MPS / NR == m) {
+            if (r < WI) fan[r] = rd_a(rch, rkk, r);
+            else fbn[r - WI] = rd_b(rch, rkk, r - WI);
+          }
       }
       __builtin_amdgcn_sched_barrier(0);
       acc[m / JT][m % JT] =
@@ -706,9 +714,10 @@ void conv3x3_u8s8_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 template <class CA, class CB>
 struct PairCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
-  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles");
+  // (the wave tiles of A and B may differ — e.g. the 8-wave one-image conv3+4
+  // of small batches: A 64 couts x 64 pixels, B 32 couts x 128 pixels)
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
-                CA::W == CB::W && CA::WI == CB::WI, "same whole-image tiling");
+                CA::W == CB::W && !CA::kBand && !CB::kBand, "same whole-image tiling");
   static constexpr int MAIN_A = CA::PATCH + 3 * CA::WBUF;
   static constexpr int MAIN_B = CB::PATCH + 3 * CB::WBUF;
   static constexpr int MAIN = MAIN_A > MAIN_B ? MAIN_A : MAIN_B;
@@ -726,7 +735,7 @@ struct PairCfg {
 // A's epilogue into B's LDS patch (zero-point halo, then the requantized
 // interior as q - 128).  Shared by both pair bodies.
 template <class CA, class CB>
-QCN_DEV void pair_handoff(v16i (&acc)[CA::WI][4], const ConvEpi& epa, const float* eka, int xb_zp,
+QCN_DEV void pair_handoff(v16i (&acc)[CA::WI][CA::JT], const ConvEpi& epa, const float* eka, int xb_zp,
                           uint8_t* lds, int wave, int lane, int tid) {
   const uint32_t padw = xor80(splat_u8(xb_zp));
   const uint4 pad4 = make_uint4(padw, padw, padw, padw);
@@ -748,8 +757,8 @@ QCN_DEV void pair_handoff(v16i (&acc)[CA::WI][4], const ConvEpi& epa, const floa
     const int co_base = wc * 32 * CA::WI + i * 32;
     const EpiK K = load_epik_lds(eka, CA::kCout, co_base, hi);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = (wp * 4 + j) * 32 + l32;
+    for (int j = 0; j < CA::JT; ++j) {
+      const int m = (wp * CA::JT + j) * 32 + l32;
       const int seg = m / (CA::R * CA::W), row = (m / CA::W) % CA::R, col = m % CA::W;
       epilogue_tile_kf<1, true, true>(&acc[i][j], K, epa, co_base, hi,
                                       lds + CB::slot(seg, row + 1, col + 1));
@@ -778,15 +787,21 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
   stage_patch<CA, BYPASS_L1>(x, nimg, x_zp, n0, y0, lds, tid);
 
-  v16i acc[CA::WI][4];
+  v16i acc[CA::WI][CA::JT];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
 
   // A's epilogue into B's patch (A's patch and ring are dead past the main
   // loop's final barrier)
   pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
   __syncthreads();
-  conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
-  conv_epilogue<CB, WT>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+  if constexpr (CA::WI == CB::WI && CA::JT == CB::JT) {
+    conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
+    conv_epilogue<CB, WT>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+  } else {
+    v16i accb[CB::WI][CB::JT];
+    conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, accb);
+    conv_epilogue<CB, WT>(accb, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+  }
 }
 
 template <class CA, class CB>
@@ -907,7 +922,7 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
 template <class CA, class CB>
 struct PairGaCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
-  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles");
+  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles (the GA loop)");
   // (B may own a slice of the couts with a narrower wave tile: the patch
   // layout depends only on B's input side)
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
@@ -1948,6 +1963,16 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     static const int off34 = env_int("QCN_DUAL_OFFSET34", 2);
     if (impl34 == 12) return launch_pair_dual<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
     if (impl34 == 13) return launch_pair_dual<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
+    // one image per CU or fewer (config 2): eight waves per image — conv3 as
+    // 64-cout x 64-pixel wave tiles, conv4 as 32-cout x 128-pixel tiles — so
+    // each SIMD holds two waves of the image's work instead of one
+    // (QCN_SMALL34: images per CU at or below which; 0 = never)
+    static const int small34 = env_int("QCN_SMALL34", 1);
+    const int ncu34 = qcn_cu_count();
+    if (impl34 == 0 && ncu34 > 0 && nimg <= small34 * ncu34)
+      return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
+                         ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 2) return launch_pair_ga<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 3) return launch_pair_ga<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 4) return launch_pair_ga<A3, B4, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
