@@ -74,7 +74,9 @@ HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
-                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel"),
+                  # (one form runs per batch size: the split form at <= 1 image per CU)
+                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel",
+                             "convpair_ga_split_kernel"),
                   "conv3456": ("conv3456_kernel",),
                   # "fc_finish" matches fc_finish_kernel (static) and fc_finish_qdq_kernel (QDQ)
                   "fc12": ("fc_splitk_kernel", "fc_finish"),

@@ -998,16 +998,15 @@ void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 // the pair costs 4/3 of the MFMAs in twice the workgroups.  B's wave tile is
 // narrower (CB::WI) so four waves still cover the slice.
 template <class CA, class CB, int D, int COUTB>
-__global__ __launch_bounds__(CA::NT, 2)
-void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                              const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
-                              const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+QCN_DEV void convpair_ga_split_body(int blk, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                                    const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                                    const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   using P = PairGaCfg<CA, CB>;
   static_assert(COUTB % CB::kCout == 0 && CA::NWAVES == CB::NWAVES, "cout slices");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NS = COUTB / CB::kCout;
-  const int tile = (int)blockIdx.x / NS, co0 = ((int)blockIdx.x % NS) * CB::kCout;
+  const int tile = blk / NS, co0 = (blk % NS) * CB::kCout;
   ConvEpi eph = epb;   // this slice's constants
   eph.u += co0; eph.v += co0; eph.mult += co0; eph.corr += co0;
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
@@ -1031,6 +1030,14 @@ void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   v16i accb[CB::WI][4];
   conv_mainloop_ga<CB, D, CSTB>(lds, wb, eph.corr, wave, lane, accb, gb, WgBar{}, co0);
   conv_epilogue<CB, true>(accb, eph, lds, nimg, wave, lane, tid, y, tile, ekb, WgBar{}, co0, COUTB);
+}
+
+template <class CA, class CB, int D, int COUTB>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                              const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                              const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  convpair_ga_split_body<CA, CB, D, COUTB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
 // --------------------------------------------------------------------------

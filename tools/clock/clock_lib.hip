@@ -50,6 +50,17 @@ void convpair_stamped(int kind, const uint8_t* __restrict__ x, int nimg, int x_z
   clk_store(kind, t0, r0);
 }
 
+template <class CA, class CB, int D, int COUTB>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_ga_split_stamped(int kind, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                               const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                               const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  convpair_ga_split_body<CA, CB, D, COUTB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  clk_store(kind, t0, r0);
+}
+
 template <class CA, class CB, int D>
 __global__ __launch_bounds__(CA::NT, 2)
 void convpair_ga_stamped(int kind, const uint8_t* __restrict__ x, int nimg, int x_zp,
@@ -127,14 +138,35 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     epb.s1 = qdqb->s1; epb.z1 = qdqb->z1; epb.inv2 = qdqb->inv2; epb.z2 = qdqb->z2;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (hw == 16 && cin == 64 && cmid == 128 && cout == 128)
+  // the product's default forms (qcn_conv3x3_pair_u8s8): at <= 1 image per
+  // CU conv3+4 on eight waves per image and the cout-split conv5+6
+  const int ncu = qcn_cu_count();
+  const bool small = ncu > 0 && nimg <= ncu;
+  if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
+    if (small)
+      return launch_pair_stamped<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
+                                 ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
+          1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair_stamped<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                                ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256)   // the product's default form
-    return launch_pair_ga_stamped<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
-                                  ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>, 4>(
+  }
+  if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
+    using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
+    if (small) {
+      using BS = ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>;
+      using P = PairGaCfg<A1, BS>;
+      const int grid = (int)(((long)nimg * A1::IMG + A1::PXB - 1) / A1::PXB) * 2;
+      auto k = convpair_ga_split_stamped<A1, BS, 4, 256>;
+      static bool attr_done[QCN_MAX_DEV] = {};
+      if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+      hipLaunchKernelGGL(k, dim3(grid), dim3(A1::NT), P::LDS, st, 2, x, nimg, x_zp, wa_packed, epa,
+                         xb_zp, wb_packed, epb, y);
+      return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+    }
+    return launch_pair_ga_stamped<A1, ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>, 4>(
         2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+  }
   return QCN_ERR_UNSUPPORTED;
 }
 

@@ -42,6 +42,8 @@ def grid_of(name, n, ncu):
         return min(n, ncu)
     if name == "conv34":
         return n                       # one 16x16 image (256 pixels) per 4-wave workgroup
+    if n <= ncu:                       # cout-split: two workgroups per pair of images
+        return 2 * ((n + 1) // 2)
     return (n + 1) // 2                # two 8x8 images per 4-wave workgroup (convpair_ga_kernel)
 
 
@@ -104,7 +106,10 @@ def main():
             clock = float(np.median(ghz))
             # MFMA cycles per SIMD of one workgroup (its images' MACs over its 4 SIMDs)
             img_per_wg = B / g
-            mfma_cyc_wg = bench.MAC_PER_IMAGE[n] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)
+            mac_wg = bench.MAC_PER_IMAGE[n] * img_per_wg
+            if n == "conv56" and B <= ncu:   # cout-split: conv5 of two images + half of conv6's
+                mac_wg = 2 * (bench.MAC_PER_IMAGE["conv5"] + bench.MAC_PER_IMAGE["conv6"] / 2)
+            mfma_cyc_wg = mac_wg / (4 * MFMA_MAC_PER_CLK_SIMD)
             rec.update({"clock_ghz": clock, "clock_ghz_p10": float(np.percentile(ghz, 10)),
                         "clock_ghz_p90": float(np.percentile(ghz, 90)),
                         "workgroups": int(g), "wg_cycles_median": float(np.median(cyc[ok])),
