@@ -991,6 +991,105 @@ void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 }
 
 // --------------------------------------------------------------------------
+// Persistent pair with the next image's patch prefetched (conv3+conv4): each
+// workgroup takes tiles blockIdx.x, + gridDim.x, ...  The interior bytes of
+// the next tile's input patch (one whole image: CA::R x CA::W pixels) are
+// loaded into registers right after conv B's first weight loads — plain
+// loads the compiler counts, so B's loop waits only for its own — and land
+// in LDS (q ^ 0x80, plus the zero-point halo) after this tile's output is
+// stored: only the first tile pays the staging latency.
+template <class C>
+struct PatchPf {
+  static constexpr int PIECES = C::R * C::W * (C::kCin / 16);   // 16-B interior pieces
+  static constexpr int PER = (PIECES + C::NT - 1) / C::NT;
+  static_assert(C::SEGS == 1 && C::R == C::H && !C::kBand, "one whole image per tile");
+  uint4 v[PER];
+};
+
+template <class C>
+QCN_DEV void patch_pf_load(PatchPf<C>& pf, const uint8_t* __restrict__ x, int nimg, int n, int tid) {
+  constexpr int CH16 = C::kCin / 16;
+  const int nc = n < nimg ? n : nimg - 1;   // (past the end: a valid dummy image)
+  const uint8_t* img = x + (long)nc * C::IMG * C::kCin;
+#pragma unroll
+  for (int k = 0; k < PatchPf<C>::PER; ++k) {
+    int e = tid + k * C::NT;
+    e = e < PatchPf<C>::PIECES ? e : 0;
+    pf.v[k] = *reinterpret_cast<const uint4*>(img + (long)(e / CH16) * C::kCin + (e % CH16) * 16);
+  }
+}
+
+template <class C>
+QCN_DEV void patch_pf_store(const PatchPf<C>& pf, int x_zp, uint8_t* patch, int tid) {
+  constexpr int CH16 = C::kCin / 16;
+#pragma unroll
+  for (int k = 0; k < PatchPf<C>::PER; ++k) {
+    const int e = tid + k * C::NT;
+    if (e < PatchPf<C>::PIECES) {
+      const int px = e / CH16, chunk = e % CH16;
+      const uint4 v = pf.v[k];
+      *reinterpret_cast<uint4*>(patch + C::slot(0, px / C::W + 1, px % C::W + 1) + chunk * 16) =
+          make_uint4(xor80(v.x), xor80(v.y), xor80(v.z), xor80(v.w));
+    }
+  }
+  // zero-point halo: rows 0 and R+1, columns 0 and W+1
+  const uint32_t padw = xor80(splat_u8(x_zp));
+  constexpr int HALO = 2 * C::PCOLS + 2 * C::R;
+  for (int e = tid; e < HALO * CH16; e += C::NT) {
+    const int hs = e / CH16, chunk = e % CH16;
+    int pr, pc;
+    if (hs < C::PCOLS) { pr = 0; pc = hs; }
+    else if (hs < 2 * C::PCOLS) { pr = C::PROWS - 1; pc = hs - C::PCOLS; }
+    else { const int r = hs - 2 * C::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? C::PCOLS - 1 : 0; }
+    *reinterpret_cast<uint4*>(patch + C::slot(0, pr, pc) + chunk * 16) = make_uint4(padw, padw, padw, padw);
+  }
+}
+
+template <class CA, class CB, int D>
+__global__ __launch_bounds__(CA::NT, 2)
+void convpair_pipe_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
+                          const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
+                          const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
+  using P = PairGaCfg<CA, CB>;
+  static_assert(CA::PXB == CA::IMG, "one image per tile");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  const int tid0 = threadIdx.x;
+  stage_epik<CA::kCout, CA::NT>(epa, eka, tid0);
+  stage_epik<CB::kCout, CB::NT>(epb, ekb, tid0);
+  const int G = (int)gridDim.x;
+  int t = (int)blockIdx.x;
+  if (t >= nimg) return;
+  stage_patch<CA>(x, nimg, x_zp, t, 0, lds, tid0);
+  for (; t < nimg; t += G) {
+    // laundered per tile (nothing thread-id-derived hoisted across the loop)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6;
+    GaFrag<CA, D> ga;
+    ga_prefetch<CA, D>(ga, wa, wave, lane);
+    __syncthreads();   // this tile's patch complete
+    v16i acc[CA::WI][CA::JT];
+    conv_mainloop_ga<CA, D>(lds, wa, epa.corr, wave, lane, acc, ga);
+    GaFrag<CB, D> gb;
+    ga_prefetch<CB, D>(gb, wb, wave, lane);
+    const bool more = t + G < nimg;
+    PatchPf<CA> pf;
+    if (more) patch_pf_load<CA>(pf, x, nimg, t + G, tid);
+    pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
+    __syncthreads();
+    v16i accb[CB::WI][CB::JT];
+    conv_mainloop_ga<CB, D>(lds, wb, epb.corr, wave, lane, accb, gb);
+    conv_epilogue<CB, true>(accb, epb, lds, nimg, wave, lane, tid, y, t, ekb);
+    if (more) {
+      __syncthreads();   // the staged output is read out before the next patch overwrites it
+      patch_pf_store<CA>(pf, x_zp, lds, tid);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
 // Small batches (config 2, batch 256: 128 two-image workgroups on 256 CUs):
 // workgroup 2t + h owns images 2t, 2t+1 and conv B's output channels
 // [h * CB::kCout, (h + 1) * CB::kCout) of a COUTB-channel layer.  Each of the
@@ -1805,6 +1904,21 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+template <class CA, class CB, int D>
+int launch_pair_pipe(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
+                     int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st,
+                     int wg_per_cu) {
+  using P = PairGaCfg<CA, CB>;
+  const int ncu = qcn_cu_count();
+  if (ncu <= 0) return QCN_ERR_HIP;
+  const int grid = nimg < wg_per_cu * ncu ? nimg : wg_per_cu * ncu;
+  auto k = convpair_pipe_kernel<CA, CB, D>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 template <class CA, class CB, int D, int COUTB>
 int launch_pair_ga_split(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
                          int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
@@ -1980,6 +2094,8 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
       return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (impl34 == 22) return launch_pair_pipe<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, 2);
+    if (impl34 == 23) return launch_pair_pipe<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, 2);
     if (impl34 == 2) return launch_pair_ga<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 3) return launch_pair_ga<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     if (impl34 == 4) return launch_pair_ga<A3, B4, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
