@@ -369,12 +369,11 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // A operand: row wc*32*WI + 32i + l32, 16-B slot (2kk + hi) ^ swizzle
   const int arow = wc * 32 * WI + l32;
   const int aswz = (arow >> 2) & 3;  // same for arow + 32i
+  // the zero-point correction is the first K-step's C operand (no copies
+  // into the JT accumulator tiles)
+  v16i c0[WI];
 #pragma unroll
-  for (int i = 0; i < WI; ++i) {
-    const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
-#pragma unroll
-    for (int j = 0; j < JT; ++j) acc[i][j] = c0;
-  }
+  for (int i = 0; i < WI; ++i) c0[i] = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // patch + corr loads retired
 #pragma unroll
   for (int g = 0; g < C::NG; ++g) issue_g(0, g);
@@ -401,7 +400,7 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   // one step: MPS MFMAs on (fa, fb); reads of step (rch, rkk) into (fan, fbn)
   // interleaved one per MFMA; DMA pieces of chunk dch spread over the MFMAs
   auto step = [&](v4i (&fan)[WI], v4i (&fbn)[JT], int rch, int rkk, bool rd,
-                  const v4i (&fa)[WI], const v4i (&fb)[JT], bool dma, int dch) {
+                  const v4i (&fa)[WI], const v4i (&fb)[JT], bool dma, int dch, bool first) {
 #pragma unroll
     for (int m = 0; m < MPS; ++m) {
       if (rd) {
@@ -417,8 +416,8 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
           }
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[m / JT][m % JT] =
-          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / JT], fb[m % JT], acc[m / JT][m % JT], 0, 0, 0);
+      acc[m / JT][m % JT] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+          fa[m / JT], fb[m % JT], first ? c0[m / JT] : acc[m / JT][m % JT], 0, 0, 0);
 #pragma unroll
       for (int g = 0; g < C::NG; ++g)
         if (dma && m == (2 * g + 1) * MPS / (2 * C::NG)) {
@@ -469,13 +468,13 @@ QCN_DEV void conv_mainloop(const uint8_t* patch, uint8_t* wring, const int8_t* _
   for (int ch = 0; ch < C::NCH; ++ch) {
     if (lag && ch + 1 < C::NCH) ring_barrier();
     // step (ch, 0): read (ch, 1), multiply (ch, 0)
-    step(fa1, fb1, ch, 1, true, fa0, fb0, lag && ch + 2 < C::NCH, ch + 2);
+    step(fa1, fb1, ch, 1, true, fa0, fb0, lag && ch + 2 < C::NCH, ch + 2, ch == 0);
     if (ch + 1 < C::NCH) {
       // step (ch, 1): chunk ch+1 landed and visible -> read (ch+1, 0), multiply (ch, 1)
       if (!lag) ring_barrier();   // chunk ch-1's reads stay before the barrier
-      step(fa0, fb0, ch + 1, 0, true, fa1, fb1, !lag && ch + 2 < C::NCH, ch + 2);
+      step(fa0, fb0, ch + 1, 0, true, fa1, fb1, !lag && ch + 2 < C::NCH, ch + 2, false);
     } else {
-      step(fa0, fb0, 0, 0, false, fa1, fb1, false, 0);
+      step(fa0, fb0, 0, 0, false, fa1, fb1, false, 0, false);
     }
   }
   // every wave's last reads are consumed; the caller reuses the LDS
@@ -872,12 +871,9 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
   const PatchAddr<C> pa(wp, l32, hi);
   const wt_rsrc_t wr = wt_rsrc(wpk);
   const int voff = ga_voff<C>(wave, lane) + co0 * 64;
+  v16i c0[WI];   // the first K-step's C operand
 #pragma unroll
-  for (int i = 0; i < WI; ++i) {
-    const v16i c0 = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
-  }
+  for (int i = 0; i < WI; ++i) c0[i] = acc_init_corr(corr, wc * 32 * WI + i * 32, hi);
   auto rd_b = [&](int s, int j) {
     const int ch = s >> 1, kk = s & 1;
     const int tap = ch / CB, cb = ch % CB;
@@ -896,8 +892,8 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
       constexpr int BSP = MPS / 4;
       if (s + 1 < S && m % BSP == 0) fb[(s + 1) & 1][m / BSP] = rd_b(s + 1, m / BSP);
       __builtin_amdgcn_sched_barrier(0);
-      acc[m / 4][m % 4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(g.fa[s % (D + 1)][m / 4], fb[s & 1][m % 4],
-                                                                acc[m / 4][m % 4], 0, 0, 0);
+      acc[m / 4][m % 4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+          g.fa[s % (D + 1)][m / 4], fb[s & 1][m % 4], s == 0 ? c0[m / 4] : acc[m / 4][m % 4], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + D < S && m == MPS / 2 - 1) {
         // slot (s + D) % (D + 1) == (s - 1) % (D + 1): consumed by step s - 1
@@ -1393,12 +1389,9 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
   const PatchAddr<C> pa(wp, l32, hi);
   const int arow = wc * 64 + l32;
   const int aswz = (arow >> 2) & 3;
+  v16i c0[2];   // the first K-step's C operand
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const v16i c0 = acc_init_corr(corr, wc * 64 + i * 32, hi);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = c0;
-  }
+  for (int i = 0; i < 2; ++i) c0[i] = acc_init_corr(corr, wc * 64 + i * 32, hi);
   const uint8_t* abase = wres + arow * 64;
   auto rd_a = [&](int ch, int kk, int i) {
     return *reinterpret_cast<const v4i*>(abase + ch * C::WBUF + i * 32 * 64 +
@@ -1410,7 +1403,7 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
                                          kk * 32);
   };
   auto step = [&](v4i (&fan)[2], v4i (&fbn)[4], int rch, int rkk, bool rd,
-                  const v4i (&fa)[2], const v4i (&fb)[4]) {
+                  const v4i (&fa)[2], const v4i (&fb)[4], bool first) {
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       if (rd) {
@@ -1418,8 +1411,8 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
         else if (m < 6) fbn[m - 2] = rd_b(rch, rkk, m - 2);
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[m >> 2][m & 3] =
-          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m >> 2], fb[m & 3], acc[m >> 2][m & 3], 0, 0, 0);
+      acc[m >> 2][m & 3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+          fa[m >> 2], fb[m & 3], first ? c0[m >> 2] : acc[m >> 2][m & 3], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1430,8 +1423,8 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
   for (int j = 0; j < 4; ++j) fb0[j] = rd_b(0, 0, j);
 #pragma unroll
   for (int ch = 0; ch < C::NCH; ++ch) {
-    step(fa1, fb1, ch, 1, true, fa0, fb0);
-    step(fa0, fb0, ch + 1, 0, ch + 1 < C::NCH, fa1, fb1);
+    step(fa1, fb1, ch, 1, true, fa0, fb0, ch == 0);
+    step(fa0, fb0, ch + 1, 0, ch + 1 < C::NCH, fa1, fb1, false);
   }
 }
 

@@ -21,6 +21,7 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace qcn {
@@ -72,9 +73,11 @@ struct GemmArgs {
   uint8_t* y;
 };
 
-template <int BN>
+template <int BN, int BM_ = 256>
 struct GemmCfg {
-  static constexpr int BM = 256;
+  // BM_ = 128 (thin convs, K <= 256): half the pixels per tile, 64 accumulators
+  // per wave and a third of the LDS, so three workgroups share a CU
+  static constexpr int BM = BM_;
   static constexpr int NW = BN == 256 ? 8 : 4;   // waves (BN = 256: 512 threads, one per CU)
   static constexpr int NT = 64 * NW;
   static constexpr int WN = BN / 64;          // waves along channels
@@ -88,6 +91,7 @@ struct GemmCfg {
   static constexpr int D = DA + NB;
   static constexpr int OS = BN + 16;          // output staging row stride (bytes)
   static constexpr int LDS = 3 * STAGE;
+  static constexpr int MINW = BM == 128 ? 3 : 512 / NT;   // waves per SIMD the registers allow
   static_assert(FA % NW == 0, "A fragments split evenly over the waves");
   static_assert(BM * OS <= LDS, "output staging fits in the ring");
 };
@@ -104,9 +108,9 @@ struct KCursor {
   }
 };
 
-template <int BN, bool RESID>
-__global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_gemm_kernel(GemmArgs a) {
-  using C = GemmCfg<BN>;
+template <int BN, bool RESID, int BM = 256>
+__global__ __launch_bounds__((GemmCfg<BN, BM>::NT), (GemmCfg<BN, BM>::MINW)) void conv_gemm_kernel(GemmArgs a) {
+  using C = GemmCfg<BN, BM>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -195,17 +199,18 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   };
 
   const int wc = wave % C::WN, wm = wave / C::WN;
+  // accumulators: the first half-stage's MFMAs take the zero-point
+  // correction cinit[i] as their C operand (no copies into 2 x JT tiles:
+  // those v_movs were ~10 % of a K = 64 conv's VALU)
   v16i acc[2][C::JT];
+  v16i cinit[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    v16i c0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int4 c4 = *reinterpret_cast<const int4*>(a.corr + n0 + wc * 64 + i * 32 + 8 * g + 4 * hi);
-      c0[4 * g] = c4.x; c0[4 * g + 1] = c4.y; c0[4 * g + 2] = c4.z; c0[4 * g + 3] = c4.w;
+      cinit[i][4 * g] = c4.x; cinit[i][4 * g + 1] = c4.y; cinit[i][4 * g + 2] = c4.z; cinit[i][4 * g + 3] = c4.w;
     }
-#pragma unroll
-    for (int j = 0; j < C::JT; ++j) acc[i][j] = c0;
   }
   // Residual join (RESID): the identity bytes each thread's join rows need
   // (thread (rr, cq): 16 channels of rows rr + R_RPI it, see the epilogue).
@@ -251,8 +256,8 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   // ring's one barrier per stage sits between its two halves: it certifies
   // stage st+1 landed (its reads start in the second half) and that every
   // wave is done with stage st-1, whose buffer stage st+2's DMA then reuses.
-  auto seg = [&](const v4i (&fa)[2], v4i (&fb)[C::JT], v4i (&na)[2], v4i (&nb)[C::JT], int rst,
-                 int rc, bool rd) {
+  auto seg = [&](auto first, const v4i (&fa)[2], v4i (&fb)[C::JT], v4i (&na)[2], v4i (&nb)[C::JT],
+                 int rst, int rc, bool rd) {
 #pragma unroll
     for (int j = 0; j < C::JT; ++j)
 #pragma unroll
@@ -264,8 +269,12 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
         else if (m < 2 + C::JT) nb[m - 2] = rd_b(rst, rc, m - 2);
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[m / C::JT][m % C::JT] =
-          __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / C::JT], fb[m % C::JT], acc[m / C::JT][m % C::JT], 0, 0, 0);
+      if constexpr (decltype(first)::value)
+        acc[m / C::JT][m % C::JT] =
+            __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / C::JT], fb[m % C::JT], cinit[m / C::JT], 0, 0, 0);
+      else
+        acc[m / C::JT][m % C::JT] =
+            __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[m / C::JT], fb[m % C::JT], acc[m / C::JT][m % C::JT], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -284,9 +293,10 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   for (int i = 0; i < 2; ++i) fa0[i] = rd_a(0, 0, i);
 #pragma unroll
   for (int j = 0; j < C::JT; ++j) fb0[j] = rd_b(0, 0, j);
-  for (int st = 0; st < nst; ++st) {
-    // first half: multiply (st, 0), read (st, 1)
-    seg(fa0, fb0, fa1, fb1, st, 1, true);
+  // stage st: first half multiplies (st, 0) and reads (st, 1); the stage
+  // barrier; second half multiplies (st, 1) and reads (st+1, 0).  Stage 0's
+  // first half is peeled (its MFMAs start from cinit).
+  auto mid = [&](int st) {
     __builtin_amdgcn_sched_barrier(0);
     const bool more = st + 1 < nst;
     if (more) {
@@ -298,8 +308,13 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
       if (st + 2 < nst) issue(st + 2);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // second half: multiply (st, 1), read (st+1, 0)
-    seg(fa1, fb1, fa0, fb0, st + 1, 0, more);
+    seg(std::false_type{}, fa1, fb1, fa0, fb0, st + 1, 0, more);
+  };
+  seg(std::true_type{}, fa0, fb0, fa1, fb1, 0, 1, true);
+  mid(0);
+  for (int st = 1; st < nst; ++st) {
+    seg(std::false_type{}, fa0, fb0, fa1, fb1, st, 1, true);
+    mid(st);
   }
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();   // every wave is done with the ring: reuse it
@@ -439,15 +454,15 @@ __global__ __launch_bounds__(GemmCfg<BN>::NT, 512 / GemmCfg<BN>::NT) void conv_g
   }
 }
 
-template <int BN, bool RESID>
+template <int BN, bool RESID, int BM = 256>
 int launch_gemm(GemmArgs& a, hipStream_t st) {
-  using C = GemmCfg<BN>;
+  using C = GemmCfg<BN, BM>;
   a.mt = (int)((a.npix + C::BM - 1) / C::BM);
   a.nt = a.cout / BN;
   static bool attr_done[QCN_MAX_DEV] = {};
-  if (!qcn_set_lds_once((const void*)conv_gemm_kernel<BN, RESID>, C::LDS, attr_done))
+  if (!qcn_set_lds_once((const void*)conv_gemm_kernel<BN, RESID, BM>, C::LDS, attr_done))
     return QCN_ERR_HIP;
-  hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID>), dim3(a.mt * a.nt), dim3(C::NT), C::LDS, st, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<BN, RESID, BM>), dim3(a.mt * a.nt), dim3(C::NT), C::LDS, st, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
@@ -492,6 +507,15 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   // (profiles/r02_diag_resnet_bn256_layers.txt)
   if (cout % 256 == 0 && !resid && (kh * kw > 1 || cin >= 2048))
     return qcn::launch_gemm<256, false>(a, st);
+  // thin convs (K <= QCN_GEMM_THIN_K) on 128-pixel tiles, three workgroups per
+  // CU. Off by default: the layer-1 expand 1x1s (K = 64) went 0.236 -> 0.278 ms
+  // on them, ResNet-50 100.8 -> 96.0 K img/s (profiles/r03_diag_resnet_thin_ab.txt)
+  static const int thin_k = [] {
+    const char* e = std::getenv("QCN_GEMM_THIN_K");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (cout % 128 == 0 && a.kcs * 32 <= thin_k)
+    return resid ? qcn::launch_gemm<128, true, 128>(a, st) : qcn::launch_gemm<128, false, 128>(a, st);
   if (cout % 128 == 0)
     return resid ? qcn::launch_gemm<128, true>(a, st) : qcn::launch_gemm<128, false>(a, st);
   return resid ? qcn::launch_gemm<64, true>(a, st) : qcn::launch_gemm<64, false>(a, st);
