@@ -71,6 +71,9 @@ struct GemmArgs {
   float s3, s_r, inv_o;
   int z_r, z_o;
   uint8_t* y;
+  // streaming 1x1 kernel: 32-pixel strips, chunks of `per` strips, `cg`
+  // channel groups of NW x 32 output channels
+  int nstrip, nchunk, per, cg;
 };
 
 template <int BN, int BM_ = 256>
@@ -466,6 +469,369 @@ int launch_gemm(GemmArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+QCN_DEV void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// raw buffer descriptor (wave-uniform base, 2 GiB range, no stride)
+QCN_DEV v4i buf_rsrc(const void* base) {
+  const uint64_t p = (uint64_t)(uintptr_t)base;
+  return (v4i){(int)(uint32_t)p, (int)((uint32_t)(p >> 32) & 0xffff), 0x7fffffff, 0x00020000};
+}
+// 16-B buffer load / store issued from inline asm: invisible to the
+// compiler's wait-count pass, so the caller counts vmcnt itself
+QCN_DEV v4i asm_bload(v4i rs, int voff) {
+  v4i r;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rs) : "memory");
+  return r;
+}
+QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
+  // s_nop: a VALU write of a >8-byte store's data VGPR right behind the store
+  // needs a wait state (the hazard recognizer does not see inside asm)
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" :: "v"(d), "v"(voff), "s"(rs) : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Streaming 1x1 conv (stride 1, no padding, K = Cin <= 256): the bottleneck's
+// thin expand / reduce convs move 16-32 output bytes (plus 16 identity bytes
+// for the join) per 64-256 MACs, so they are HBM-bound, and the tiled kernel
+// above — load a stage, multiply, requantize, store, one tile per workgroup
+// residency — leaves HBM idle during each tile's epilogue.  Here every wave
+// owns one 32-channel output tile for good: its A fragments (the channel
+// tile's weights, K/32 x 16 B per lane) and epilogue constants stay in
+// registers, and it walks a chunk of 32-pixel strips with the next P strips'
+// activations and identity bytes already in flight.  The NW waves of a
+// workgroup (and the cg workgroups of a chunk, all placed on one XCD) read the
+// same strips, so each activation byte leaves HBM once.
+//
+// Activations (B fragments) come either straight into registers (BL = false:
+// K/32 16-B loads per lane and strip), or (BL = true, K = 256: eight 1-KiB
+// pieces per strip that every wave would otherwise fetch itself) through an
+// LDS ring filled by LDS-DMA, each wave loading K/32/NW pieces of whole pixel
+// rows; the row's 16-B chunks are XOR-swizzled by pixel so the MFMA's
+// lane-linear fragment reads are conflict-free.
+//
+// Per strip: K/32 MFMAs, the FBGEMM requant of 16 values per lane, two rounds
+// of v_permlane32_swap (MFMA layout -> 16 consecutive channels per lane), and
+// an LDS transpose of the workgroup's NW x 32 channels: a store of the MFMA
+// layout is 32 rows x 32 B per instruction, which runs the address path at
+// ~3x the work per byte of whole lines (3.8 vs 5.8 TB/s on this conv's
+// traffic, tools/micro/stream_shape.hip; 1.5x fetch and 1.3x write
+// amplification), so each wave moves 32/NW whole row segments of NW x 32 B
+// instead.  With RESID the join of custom_quantization_model.py:94-101 runs on
+// those row segments with the same fp32 op sequence as the tiled kernel's
+// join (bit-identical).
+//
+// Epilogue modes (uniform per launch, so compiled in): RQ 0 = zp_y 0 and no
+// ReLU floor (v_cvt_pk_u8_f32 alone rounds and saturates), 1 = no ReLU floor
+// (rint + zp, then the saturating pack), 2 = general clamp; ZO (RESID) = the
+// join's output zero point is 0 (ReLU = saturation at 0).
+
+// vmcnt bound at a wait of the strip loop, from the issue order: prologue
+// B(j) x NB, I(j) for j < P; step t issues S(t), B(t+P) x NB, I(t+P) after its
+// waits.  BL = false waits at the head of step t for B(t), I(t); BL = true
+// waits before step t's barrier for B(t+1), I(t) (t = -1: the prologue's wait
+// for B(0)).  Returns the number of younger operations that may stay in flight.
+constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t) {
+  int pos = 0, last = -1;
+  auto issue_b = [&](int strip) {
+    for (int i = 0; i < NB; ++i) {
+      if (strip == (BL ? t + 1 : t)) last = pos;
+      ++pos;
+    }
+  };
+  auto issue_i = [&](int strip) {
+    if (!RESID) return;
+    if (strip == t && !(BL && t < 0)) last = pos;
+    ++pos;
+  };
+  for (int j = 0; j < P; ++j) { issue_b(j); issue_i(j); }
+  for (int u = 0; u < t; ++u) { ++pos; issue_b(u + P); issue_i(u + P); }
+  return pos - 1 - last;
+}
+
+template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL>
+__global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_kernel(GemmArgs a) {
+  constexpr int KC = K / 32;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l32 = lane & 31, hi = lane >> 5;
+  // block -> (chunk, channel group); the cg groups of a chunk share blockIdx % 8
+  const int b = blockIdx.x, x8 = b & 7, kq = b >> 3;
+  const int cgi = kq % a.cg, c = (kq / a.cg) * 8 + x8;
+  if (c >= a.nchunk) return;
+  const int s0 = c * a.per, s1 = min(s0 + a.per, a.nstrip);
+  const int cout = a.cout, co0 = (cgi * NW + wave) * 32;
+
+  v4i wa[KC];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc)
+    wa[kc] = *reinterpret_cast<const v4i*>(a.w + ((long)kc * cout + co0 + l32) * 32 + hi * 16);
+  // constants of the lane's channels co0 + 8g + 4hi + e
+  v16i corr;
+  v2f u[8], v[8], m[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int co = co0 + 8 * g + 4 * hi;
+    const int4 c4 = *reinterpret_cast<const int4*>(a.corr + co);
+    corr[4 * g] = c4.x; corr[4 * g + 1] = c4.y; corr[4 * g + 2] = c4.z; corr[4 * g + 3] = c4.w;
+    const float4 x4 = *reinterpret_cast<const float4*>(a.u + co);
+    const float4 y4 = *reinterpret_cast<const float4*>(a.v + co);
+    const float4 z4 = *reinterpret_cast<const float4*>(a.mult + co);
+    u[2 * g] = (v2f){x4.x, x4.y}; u[2 * g + 1] = (v2f){x4.z, x4.w};
+    v[2 * g] = (v2f){y4.x, y4.y}; v[2 * g + 1] = (v2f){y4.z, y4.w};
+    m[2 * g] = (v2f){z4.x, z4.y}; m[2 * g + 1] = (v2f){z4.z, z4.w};
+  }
+  // the constants land before the strip loop (otherwise the compiler's wait
+  // for them sits inside the loop as a vmcnt(0) that drains the prefetch)
+#pragma unroll
+  for (int h = 0; h < 8; ++h) asm volatile("" :: "v"(u[h]), "v"(v[h]), "v"(m[h]));
+  asm volatile("" :: "v"(corr));
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) asm volatile("" :: "v"(wa[kc]));
+  const float zpf = (float)a.zp_y, lof = (float)a.lo;
+  const v2f zpv = {zpf, zpf};
+  const v2f s3v = {a.s3, a.s3};
+  const v2f zr = {(float)a.z_r, (float)a.z_r}, sr = {a.s_r, a.s_r}, io = {a.inv_o, a.inv_o};
+  const float zof = (float)a.z_o;
+  const int lastp = (int)(a.npix - 1);   // npix < 2^31 - 256 (checked at the ABI)
+
+  // 32-bit buffer offsets (activations, identity and output are < 2 GiB:
+  // checked at launch).  Every memory operation is unconditional: pixel rows
+  // past the end (and strips past s1) are clamped to the last pixel, whose
+  // output they recompute bit for bit, so the duplicate stores write the same
+  // bytes.  The strip loads and stores are issued from inline asm with the
+  // waits counted here (stream_vmcnt): on a runtime-trip-count loop the
+  // compiler's own bookkeeping falls back to vmcnt(0) at the loop head, which
+  // drains the prefetch every round.
+  const v4i xr = buf_rsrc(a.x), rr = buf_rsrc(a.r), yr = buf_rsrc(a.y);
+  auto pix = [&](int st, int row) {
+    st = st < s1 ? st : s1 - 1;
+    const int p = st * 32 + row;
+    return p < lastp ? p : lastp;
+  };
+  constexpr int ROWB = NW * 32, RS = ROWB + 16, LPR = ROWB / 16, RPW = 64 / LPR;
+  static_assert(RPW * NW == 32, "each wave moves 32 / NW rows of a strip");
+  // B ring (BL): 1-KiB pieces of RPB pixel rows, CPR 16-B chunks per row
+  constexpr int CPR = K / 16, RPB = 1024 / K, NDMA = KC / NW, RING = BL ? P * 32 * K : 16;
+  static_assert(!BL || NDMA * NW == KC, "every wave loads the same number of B pieces");
+  __shared__ __attribute__((aligned(16))) uint8_t tile[2][32 * RS];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
+  const int rrow = wave * RPW + lane / LPR, rcol = (lane % LPR) * 16;
+  const int cb0 = cgi * ROWB;
+  auto swz = [](int row) { return (row / (16 / CPR)) % CPR; };
+  constexpr int NB = BL ? NDMA : KC;   // B vector-memory ops per strip and wave
+
+  v4i bq[BL ? 1 : P][KC];
+  v4i rq[P];
+  auto load = [&](int q, int st) {
+    if constexpr (BL) {
+      const int row = lane / CPR;   // row within the piece
+#pragma unroll
+      for (int j = 0; j < NDMA; ++j) {
+        const int i = wave + NW * j, r = i * RPB + row;
+        glds16(a.x + (long)pix(st, r) * K + ((lane % CPR) ^ swz(r)) * 16, ring + q * 32 * K + i * 1024);
+      }
+    } else {
+      const int xo = pix(st, l32) * K + hi * 16;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) bq[q][kc] = asm_bload(xr, xo + kc * 32);
+    }
+    if constexpr (RESID) rq[q] = asm_bload(rr, pix(st, rrow) * cout + cb0 + rcol);
+  };
+  // wait at step t (slot q): the asm ties the slot's registers, so no use of
+  // them moves above it
+  auto wait_vm = [&](auto tc, int q) {
+    constexpr int N = stream_vmcnt(P, NB, RESID, BL, decltype(tc)::value);
+    if constexpr (!BL) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) asm volatile("" : "+v"(bq[q][kc]));
+    }
+    if constexpr (RESID) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(rq[q]) : "n"(N) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+    if constexpr (!BL) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) asm volatile("" : "+v"(bq[q][kc]));
+    }
+  };
+  auto strip = [&](auto tc, int q, int st) {
+    if constexpr (!BL) wait_vm(tc, q);
+    v16i acc;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      v4i bx;
+      if constexpr (BL)
+        bx = *reinterpret_cast<const v4i*>(ring + q * 32 * K + (l32 / RPB) * 1024 +
+                                           ((l32 % RPB) * CPR + ((2 * kc + hi) ^ swz(l32))) * 16);
+      else
+        bx = bq[q][kc];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) bx[d] ^= (int)0x80808080u;   // u8 -> s8
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(wa[kc], bx, kc == 0 ? corr : acc, 0, 0, 0);
+    }
+    // FBGEMM requant (A6) of the lane's 16 channels, packed as bytes per
+    // 4-channel group g (channels 8g + 4hi + 0..3)
+    uint32_t w[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const v2f t0 = requant2(acc[4 * g], acc[4 * g + 1], u[2 * g], v[2 * g], m[2 * g]);
+      const v2f t1 = requant2(acc[4 * g + 2], acc[4 * g + 3], u[2 * g + 1], v[2 * g + 1], m[2 * g + 1]);
+      uint32_t wd;
+      if constexpr (RQ == 0) {
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(t0.x, 0, 0u);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(t0.y, 1, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(t1.x, 2, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(t1.y, 3, wd);
+      } else if constexpr (RQ == 1) {
+        const v2f r0 = (v2f){__builtin_rintf(t0.x), __builtin_rintf(t0.y)} + zpv;
+        const v2f r1 = (v2f){__builtin_rintf(t1.x), __builtin_rintf(t1.y)} + zpv;
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(r0.x, 0, 0u);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(r0.y, 1, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(r1.x, 2, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(r1.y, 3, wd);
+      } else {
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(t0.x) + zpf, lof, 255.0f), 0, 0u);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(t0.y) + zpf, lof, 255.0f), 1, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(t1.x) + zpf, lof, 255.0f), 2, wd);
+        wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(t1.y) + zpf, lof, 255.0f), 3, wd);
+      }
+      w[g] = wd;
+    }
+    // low lanes: c0-3 | c8-11 | c16-19 | c24-27 ; high lanes: c4-7 | c12-15 | ...
+    auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
+    auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
+    w[0] = s01[0]; w[1] = s01[1]; w[2] = s23[0]; w[3] = s23[1];
+    auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+    auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+    w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
+    // now low lanes hold channels co0 + 0..15, high lanes co0 + 16..31
+    uint8_t* tb = tile[st & 1];
+    *reinterpret_cast<v4i*>(tb + l32 * RS + wave * 32 + 16 * hi) = (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    if constexpr (BL) wait_vm(tc, q);
+    // the tile of strip st is complete (and, BL, strip st+1's B pieces and
+    // every wave's reads of strip st's); the other tile buffer's readers
+    // (strip st-1) passed this barrier only after their reads
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    {
+      const v4i yv = *reinterpret_cast<const v4i*>(tb + rrow * RS + rcol);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) w[g] = (uint32_t)yv[g];
+    }
+    if constexpr (RESID) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t rw = (uint32_t)rq[q][g];
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const v2f yf = {(float)((w[g] >> (8 * e)) & 0xff), (float)((w[g] >> (8 * e + 8)) & 0xff)};
+          const v2f rf = {(float)((rw >> (8 * e)) & 0xff), (float)((rw >> (8 * e + 8)) & 0xff)};
+          const v2f sm = ((yf - zpv) * s3v + (rf - zr) * sr) * io;
+          if constexpr (ZO) {
+            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
+            o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
+          } else {   // relu(s) * inv == max(s * inv, 0) since inv > 0
+            o = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f), e, o);
+            o = __builtin_amdgcn_cvt_pk_u8_f32(
+                __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.y, 0.0f)) + zof, 0.0f, 255.0f), e + 1,
+                o);
+          }
+        }
+        w[g] = o;
+      }
+    }
+    asm_bstore(yr, pix(st, rrow) * cout + cb0 + rcol, (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]});
+    load(q, st + P);   // refill the slot
+  };
+#pragma unroll
+  for (int q = 0; q < P; ++q) load(q, s0 + q);
+  if constexpr (BL) {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" :: "n"(stream_vmcnt(P, NB, RESID, BL, -1)) : "memory");
+  }
+  // first round (its own wait counts), then steady rounds
+  static_for<0, P>([&](auto q) { strip(q, q, s0 + q); });
+  for (int s = s0 + P; s < s1; s += P) {
+    static_for<0, P>([&](auto q) { strip(std::integral_constant<int, P>{}, q, s + q); });
+  }
+  // drain: the last refills are never consumed; keep their registers live
+  // until they landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    if constexpr (!BL) {
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) asm volatile("" :: "v"(bq[q][kc]));
+    }
+    if constexpr (RESID) asm volatile("" :: "v"(rq[q]));
+  }
+}
+
+template <int K, int NW, bool RESID, int P, int RQ, bool ZO>
+int launch_stream(GemmArgs& a, hipStream_t st) {
+  constexpr bool BL = K == 256;
+  const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL>;
+  static int occ_dev[QCN_MAX_DEV] = {};
+  const int d = qcn_current_device(), ncu = qcn_cu_count();
+  if (d < 0 || ncu <= 0) return QCN_ERR_HIP;
+  int& occ = occ_dev[d];
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, NW * 64, 0) != hipSuccess || occ <= 0))
+    return QCN_ERR_HIP;
+  a.cg = a.cout / (32 * NW);
+  a.nstrip = (int)((a.npix + 31) / 32);
+  // one resident wave of workgroups: cg x nchunk ~ CUs x occupancy, chunks a
+  // multiple of 8 (the XCD interleave of blockIdx)
+  int nchunk = (ncu * occ) / a.cg;
+  nchunk = nchunk < 8 ? 8 : nchunk & ~7;
+  if (nchunk > a.nstrip) nchunk = a.nstrip;
+  a.per = (a.nstrip + nchunk - 1) / nchunk;
+  a.nchunk = (a.nstrip + a.per - 1) / a.per;
+  const int grid = (a.nchunk + 7) / 8 * 8 * a.cg;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), 0, st, a);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+template <int K, int NW, bool RESID, int P>
+int stream_modes(GemmArgs& a, hipStream_t st) {
+  if constexpr (RESID) {   // the join's conv has no ReLU (lo == 0)
+    const bool zo = a.z_o == 0;
+    if (a.zp_y == 0) return zo ? launch_stream<K, NW, true, P, 0, true>(a, st) : launch_stream<K, NW, true, P, 0, false>(a, st);
+    return zo ? launch_stream<K, NW, true, P, 1, true>(a, st) : launch_stream<K, NW, true, P, 1, false>(a, st);
+  } else {
+    if (a.lo == 0) return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true>(a, st)
+                                      : launch_stream<K, NW, false, P, 1, true>(a, st);
+    return launch_stream<K, NW, false, P, 2, true>(a, st);
+  }
+}
+
+// K in {64, 128, 256}; Cout % 128 == 0 (4 waves per workgroup), or Cout % 64
+// == 0 without the join (2 waves); -1 when the shape has no streaming form
+template <bool RESID>
+int dispatch_stream(GemmArgs& a, hipStream_t st) {
+  // 32-bit buffer offsets
+  if (a.npix * (long)(a.cin > a.cout ? a.cin : a.cout) >= (1L << 31) - 4096) return -1;
+  if (a.cout % 128 != 0) {
+    if (RESID || a.cout % 64 != 0) return -1;
+    switch (a.cin) {
+      case 64: return stream_modes<64, 2, false, 4>(a, st);
+      case 128: return stream_modes<128, 2, false, 3>(a, st);
+      case 256: return stream_modes<256, 2, false, 4>(a, st);
+      default: return -1;
+    }
+  }
+  switch (a.cin) {
+    case 64: return stream_modes<64, 4, RESID, 4>(a, st);
+    case 128: return stream_modes<128, 4, RESID, 3>(a, st);
+    case 256: return stream_modes<256, 4, RESID, 4>(a, st);
+    default: return -1;
+  }
+}
+
 }  // namespace qcn
 
 extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
@@ -501,6 +867,17 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
   if (a.npix >= (1L << 31) - 256) return QCN_ERR_UNSUPPORTED;   // 32-bit pixel indices in the kernel
   hipStream_t st = (hipStream_t)stream;
+  // thin 1x1 stride-1 convs (K = Cin <= QCN_GEMM_STREAM, default 256; 0 =
+  // tiled kernel only) stream: ResNet-50 98.3-99.0 -> 102.9-104.1 K img/s
+  // same box (profiles/r03_diag_resnet_stream_ab.txt)
+  static const int stream_k = [] {
+    const char* e = std::getenv("QCN_GEMM_STREAM");
+    return e ? std::atoi(e) : 256;
+  }();
+  if (cin <= stream_k && kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && pad_h == 0 && pad_w == 0) {
+    const int rc = resid ? qcn::dispatch_stream<true>(a, st) : qcn::dispatch_stream<false>(a, st);
+    if (rc >= 0) return rc;
+  }
   // 256-channel tiles (8 waves; every gathered B row serves 256 output
   // channels) where they measured faster: the 3x3 convs and the deepest 1x1
   // (-5..8 %); the residual-join convs lose 30-40 % at one workgroup per CU

@@ -137,6 +137,47 @@ def test_conv_general_oracle(dev, shape, impl):
         assert np.array_equal(fused, qref.add_relu_q(ref, s_y, zy, r, F32(0.03), 17, F32(0.05), 0))
 
 
+@pytest.mark.parametrize("shape", [
+    # n, h, w, cin, cout, zx, relu, zy, per_channel, join z_o
+    (3, 7, 9, 64, 256, 5, False, 30, True, 0),        # 189 pixels: ragged last strip
+    (2, 56, 56, 64, 256, 0, False, 0, True, 23),      # zy = 0 (cvt-only requant), z_o != 0
+    (1, 28, 29, 128, 512, 9, False, 140, False, 0),
+    (4, 14, 14, 256, 1024, 3, False, 60, True, 11),
+    (2, 17, 5, 256, 64, 200, True, 0, True, None),   # Cout 64: two waves per workgroup
+    (1, 11, 13, 64, 64, 77, True, 20, False, None),  # ReLU with zy > 0 (general clamp)
+    (1, 1, 1, 128, 128, 0, False, 5, True, 0),       # one pixel
+    (7, 31, 33, 128, 256, 130, False, 2, True, 0),   # many chunks, tail chunk shorter
+])
+def test_conv1x1_stream_oracle(dev, shape):
+    """The streaming 1x1 stride-1 kernel (conv1x1_stream_kernel: K = Cin in
+    {64, 128, 256}, weights and constants in registers, 32-pixel strips) against
+    the oracle's conv, and with the fused residual join against conv ->
+    add_relu_q."""
+    from qconvnet import ops
+    n, h, w, cin, cout, zx, relu, zy, pc, zo = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, h, w, cin)).astype(np.uint8)
+    wf = (rng.standard_normal((cout, cin, 1, 1)) * 0.05).astype(F32)
+    s_w = qref.qparams_symmetric(wf.reshape(cout, -1).min(1), wf.reshape(cout, -1).max(1))[0] if pc \
+        else qref.qparams_symmetric(wf.min(), wf.max())[0]
+    wq = qref.quantize_weight(wf, s_w)
+    b = (rng.standard_normal(cout) * 0.3).astype(F32)
+    s_x, s_y = F32(0.02), F32(0.3 if cin >= 256 else 0.15)
+    d = _layer(dev, wq, s_x, s_w, s_y, b, zx, zy, relu, (1, 1), (0, 0))
+    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d, impl="gemm").cpu().numpy()
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, relu, (1, 1), (0, 0))
+    assert np.array_equal(out, ref)
+    if n * h * w > 1:
+        assert len(np.unique(ref)) > 8, "degenerate case"
+    if zo is not None:
+        d.s_y = s_y
+        r = rng.integers(0, 256, ref.shape).astype(np.uint8)
+        fused = ops.conv(torch.from_numpy(qx).to(dev), zx, d,
+                         resid=(torch.from_numpy(r).to(dev), F32(0.03), 17, F32(0.05), zo)).cpu().numpy()
+        assert np.array_equal(fused, qref.add_relu_q(ref, s_y, zy, r, F32(0.03), 17, F32(0.05), zo))
+
+
 def test_add_relu_golden_and_ragged(dev, golden_dir):
     from qconvnet import ops
     z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
