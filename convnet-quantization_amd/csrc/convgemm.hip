@@ -497,7 +497,7 @@ QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
 }
 
 // ---------------------------------------------------------------------------
-// Streaming 1x1 conv (stride 1, no padding, K = Cin <= 256): the bottleneck's
+// Streaming 1x1 conv (stride 1, no padding, K = Cin <= 512): the bottleneck's
 // thin expand / reduce convs move 16-32 output bytes (plus 16 identity bytes
 // for the join) per 64-256 MACs, so they are HBM-bound, and the tiled kernel
 // above — load a stage, multiply, requantize, store, one tile per workgroup
@@ -624,7 +624,10 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
   const int rrow = wave * RPW + lane / LPR, rcol = (lane % LPR) * 16;
   const int cb0 = cgi * ROWB;
-  auto swz = [](int row) { return (row / (16 / CPR)) % CPR; };
+  // XOR swizzle of a row's 16-B chunks: the 16 lanes of a ds_read_b128 group
+  // (distinct pixel rows) land on distinct 16-B bank slots
+  constexpr int SD = CPR >= 16 ? 1 : 16 / CPR;
+  auto swz = [](int row) { return (row / SD) % CPR; };
   constexpr int NB = BL ? NDMA : KC;   // B vector-memory ops per strip and wave
 
   v4i bq[BL ? 1 : P][KC];
@@ -772,9 +775,8 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   }
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, bool ZO>
+template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL>
 int launch_stream(GemmArgs& a, hipStream_t st) {
-  constexpr bool BL = K == 256;
   const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL>;
   static int occ_dev[QCN_MAX_DEV] = {};
   const int d = qcn_current_device(), ncu = qcn_cu_count();
@@ -796,38 +798,47 @@ int launch_stream(GemmArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-template <int K, int NW, bool RESID, int P>
+template <int K, int NW, bool RESID, int P, bool BL>
 int stream_modes(GemmArgs& a, hipStream_t st) {
   if constexpr (RESID) {   // the join's conv has no ReLU (lo == 0)
     const bool zo = a.z_o == 0;
-    if (a.zp_y == 0) return zo ? launch_stream<K, NW, true, P, 0, true>(a, st) : launch_stream<K, NW, true, P, 0, false>(a, st);
-    return zo ? launch_stream<K, NW, true, P, 1, true>(a, st) : launch_stream<K, NW, true, P, 1, false>(a, st);
+    if (a.zp_y == 0)
+      return zo ? launch_stream<K, NW, true, P, 0, true, BL>(a, st) : launch_stream<K, NW, true, P, 0, false, BL>(a, st);
+    return zo ? launch_stream<K, NW, true, P, 1, true, BL>(a, st) : launch_stream<K, NW, true, P, 1, false, BL>(a, st);
   } else {
-    if (a.lo == 0) return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true>(a, st)
-                                      : launch_stream<K, NW, false, P, 1, true>(a, st);
-    return launch_stream<K, NW, false, P, 2, true>(a, st);
+    if (a.lo == 0) return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true, BL>(a, st)
+                                      : launch_stream<K, NW, false, P, 1, true, BL>(a, st);
+    return launch_stream<K, NW, false, P, 2, true, BL>(a, st);
   }
 }
 
-// K in {64, 128, 256}; Cout % 128 == 0 (4 waves per workgroup), or Cout % 64
-// == 0 without the join (2 waves); -1 when the shape has no streaming form
+// K in {64, 128, 256, 512}; Cout % 128 == 0 (4 waves per workgroup), or
+// Cout % 64 == 0 without the join (2 waves, K <= 256); -1 when the shape has
+// no streaming form.  Activations through the LDS ring for K >= 128 with 4
+// waves (QCN_STREAM_BL128=0: K = 128 into registers; the layer-2 expand convs
+// 0.126 -> 0.108 ms through the ring, profiles/r03_diag_resnet_stream_ab.txt).
 template <bool RESID>
 int dispatch_stream(GemmArgs& a, hipStream_t st) {
+  static const bool bl128 = [] {
+    const char* e = std::getenv("QCN_STREAM_BL128");
+    return e ? std::atoi(e) != 0 : true;
+  }();
   // 32-bit buffer offsets
   if (a.npix * (long)(a.cin > a.cout ? a.cin : a.cout) >= (1L << 31) - 4096) return -1;
   if (a.cout % 128 != 0) {
     if (RESID || a.cout % 64 != 0) return -1;
     switch (a.cin) {
-      case 64: return stream_modes<64, 2, false, 4>(a, st);
-      case 128: return stream_modes<128, 2, false, 3>(a, st);
-      case 256: return stream_modes<256, 2, false, 4>(a, st);
+      case 64: return stream_modes<64, 2, false, 4, false>(a, st);
+      case 128: return stream_modes<128, 2, false, 3, false>(a, st);
+      case 256: return stream_modes<256, 2, false, 4, true>(a, st);
       default: return -1;
     }
   }
   switch (a.cin) {
-    case 64: return stream_modes<64, 4, RESID, 4>(a, st);
-    case 128: return stream_modes<128, 4, RESID, 3>(a, st);
-    case 256: return stream_modes<256, 4, RESID, 4>(a, st);
+    case 64: return stream_modes<64, 4, RESID, 4, false>(a, st);
+    case 128: return bl128 ? stream_modes<128, 4, RESID, 4, true>(a, st) : stream_modes<128, 4, RESID, 3, false>(a, st);
+    case 256: return stream_modes<256, 4, RESID, 4, true>(a, st);
+    case 512: return stream_modes<512, 4, RESID, 3, true>(a, st);
     default: return -1;
   }
 }
@@ -867,12 +878,13 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
   if (a.npix >= (1L << 31) - 256) return QCN_ERR_UNSUPPORTED;   // 32-bit pixel indices in the kernel
   hipStream_t st = (hipStream_t)stream;
-  // thin 1x1 stride-1 convs (K = Cin <= QCN_GEMM_STREAM, default 256; 0 =
+  // thin 1x1 stride-1 convs (K = Cin <= QCN_GEMM_STREAM, default 512; 0 =
   // tiled kernel only) stream: ResNet-50 98.3-99.0 -> 102.9-104.1 K img/s
-  // same box (profiles/r03_diag_resnet_stream_ab.txt)
+  // (K <= 256) and 104.0-105.4 -> 105.9-108.3 K (K <= 512) on two boxes
+  // (profiles/r03_diag_resnet_stream_ab.txt)
   static const int stream_k = [] {
     const char* e = std::getenv("QCN_GEMM_STREAM");
-    return e ? std::atoi(e) : 256;
+    return e ? std::atoi(e) : 512;
   }();
   if (cin <= stream_k && kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && pad_h == 0 && pad_w == 0) {
     const int rc = resid ? qcn::dispatch_stream<true>(a, st) : qcn::dispatch_stream<false>(a, st);

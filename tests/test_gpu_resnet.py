@@ -147,10 +147,13 @@ def test_conv_general_oracle(dev, shape, impl):
     (1, 11, 13, 64, 64, 77, True, 20, False, None),  # ReLU with zy > 0 (general clamp)
     (1, 1, 1, 128, 128, 0, False, 5, True, 0),       # one pixel
     (7, 31, 33, 128, 256, 130, False, 2, True, 0),   # many chunks, tail chunk shorter
+    (2, 9, 7, 512, 2048, 40, False, 11, True, 0),     # K = 512: activations through the LDS ring
+    (3, 28, 28, 512, 128, 0, True, 0, True, None),
+    (1, 5, 5, 256, 256, 9, False, 3, False, 9),
 ])
 def test_conv1x1_stream_oracle(dev, shape):
     """The streaming 1x1 stride-1 kernel (conv1x1_stream_kernel: K = Cin in
-    {64, 128, 256}, weights and constants in registers, 32-pixel strips) against
+    {64, 128, 256, 512}, weights and constants in registers, 32-pixel strips) against
     the oracle's conv, and with the fused residual join against conv ->
     add_relu_q."""
     from qconvnet import ops
