@@ -555,8 +555,9 @@ constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t) {
   return pos - 1 - last;
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL>
+template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL, bool S2 = false>
 __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_kernel(GemmArgs a) {
+  static_assert(!S2 || BL, "stride 2 reads its rows through the LDS ring");
   constexpr int KC = K / 32;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -628,6 +629,16 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   // (distinct pixel rows) land on distinct 16-B bank slots
   constexpr int SD = CPR >= 16 ? 1 : 16 / CPR;
   auto swz = [](int row) { return (row / SD) % CPR; };
+  // S2 (the stride-2 downsample 1x1): output pixel (n, oy, ox) reads input
+  // pixel (n, 2 oy, 2 ox); p < 2^22 for the fp32-reciprocal divisions
+  const int ohw = a.oh * a.ow;
+  const float rohw = 1.0f / (float)ohw, rw = 1.0f / (float)a.ow;
+  auto in_pix = [&](int p) {
+    if constexpr (!S2) return p;
+    const int n = div_small(p, ohw, rohw), rem = p - n * ohw;
+    const int oy = div_small(rem, a.ow, rw), ox = rem - oy * a.ow;
+    return (n * a.h + 2 * oy) * a.w_ + 2 * ox;
+  };
   constexpr int NB = BL ? NDMA : KC;   // B vector-memory ops per strip and wave
 
   v4i bq[BL ? 1 : P][KC];
@@ -638,7 +649,7 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
 #pragma unroll
       for (int j = 0; j < NDMA; ++j) {
         const int i = wave + NW * j, r = i * RPB + row;
-        glds16(a.x + (long)pix(st, r) * K + ((lane % CPR) ^ swz(r)) * 16, ring + q * 32 * K + i * 1024);
+        glds16(a.x + (long)in_pix(pix(st, r)) * K + ((lane % CPR) ^ swz(r)) * 16, ring + q * 32 * K + i * 1024);
       }
     } else {
       const int xo = pix(st, l32) * K + hi * 16;
@@ -775,9 +786,9 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   }
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL>
+template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL, bool S2 = false>
 int launch_stream(GemmArgs& a, hipStream_t st) {
-  const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL>;
+  const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL, S2>;
   static int occ_dev[QCN_MAX_DEV] = {};
   const int d = qcn_current_device(), ncu = qcn_cu_count();
   if (d < 0 || ncu <= 0) return QCN_ERR_HIP;
@@ -798,9 +809,13 @@ int launch_stream(GemmArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-template <int K, int NW, bool RESID, int P, bool BL>
+template <int K, int NW, bool RESID, int P, bool BL, bool S2 = false>
 int stream_modes(GemmArgs& a, hipStream_t st) {
-  if constexpr (RESID) {   // the join's conv has no ReLU (lo == 0)
+  if constexpr (S2) {   // the downsample conv: no ReLU, no join
+    if (a.lo != 0) return -1;
+    return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true, true, true>(a, st)
+                       : launch_stream<K, NW, false, P, 1, true, true, true>(a, st);
+  } else if constexpr (RESID) {   // the join's conv has no ReLU (lo == 0)
     const bool zo = a.z_o == 0;
     if (a.zp_y == 0)
       return zo ? launch_stream<K, NW, true, P, 0, true, BL>(a, st) : launch_stream<K, NW, true, P, 0, false, BL>(a, st);
@@ -817,6 +832,18 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
 // no streaming form.  Activations through the LDS ring for K >= 128 with 4
 // waves (QCN_STREAM_BL128=0: K = 128 into registers; the layer-2 expand convs
 // 0.126 -> 0.108 ms through the ring, profiles/r03_diag_resnet_stream_ab.txt).
+// the stride-2 downsample 1x1 (no padding, K in {256, 512}, Cout % 128 == 0)
+inline int dispatch_stream_s2(GemmArgs& a, hipStream_t st) {
+  if (a.npix * (long)a.cout >= (1L << 31) - 4096 || (long)a.n * a.h * a.w_ * a.cin >= (1L << 31) - 4096 ||
+      a.npix >= (1L << 22) || a.cout % 128 != 0)
+    return -1;
+  switch (a.cin) {
+    case 256: return stream_modes<256, 4, false, 4, true, true>(a, st);
+    case 512: return stream_modes<512, 4, false, 3, true, true>(a, st);
+    default: return -1;
+  }
+}
+
 template <bool RESID>
 int dispatch_stream(GemmArgs& a, hipStream_t st) {
   static const bool bl128 = [] {
@@ -888,6 +915,16 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   }();
   if (cin <= stream_k && kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && pad_h == 0 && pad_w == 0) {
     const int rc = resid ? qcn::dispatch_stream<true>(a, st) : qcn::dispatch_stream<false>(a, st);
+    if (rc >= 0) return rc;
+  }
+  // the stride-2 downsample 1x1 streams too (QCN_GEMM_STREAM_S2=0: tiled)
+  static const bool stream_s2 = [] {
+    const char* e = std::getenv("QCN_GEMM_STREAM_S2");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  if (stream_s2 && cin <= stream_k && !resid && kh == 1 && kw == 1 && stride_h == 2 && stride_w == 2 &&
+      pad_h == 0 && pad_w == 0) {
+    const int rc = qcn::dispatch_stream_s2(a, st);
     if (rc >= 0) return rc;
   }
   // 256-channel tiles (8 waves; every gathered B row serves 256 output

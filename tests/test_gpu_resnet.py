@@ -181,6 +181,34 @@ def test_conv1x1_stream_oracle(dev, shape):
         assert np.array_equal(fused, qref.add_relu_q(ref, s_y, zy, r, F32(0.03), 17, F32(0.05), zo))
 
 
+@pytest.mark.parametrize("shape", [
+    # n, h, w, cin, cout, zx, zy, per_channel
+    (3, 28, 28, 256, 512, 7, 90, True),
+    (2, 14, 14, 512, 1024, 0, 0, True),
+    (3, 13, 11, 256, 128, 200, 31, False),   # odd input sides, ragged last strip
+])
+def test_conv1x1_stride2_stream_oracle(dev, shape):
+    """The stride-2 downsample 1x1 on the streaming kernel (rows of the even
+    input pixels gathered through the LDS ring) against the oracle's conv."""
+    from qconvnet import ops
+    n, h, w, cin, cout, zx, zy, pc = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, h, w, cin)).astype(np.uint8)
+    wf = (rng.standard_normal((cout, cin, 1, 1)) * 0.05).astype(F32)
+    s_w = qref.qparams_symmetric(wf.reshape(cout, -1).min(1), wf.reshape(cout, -1).max(1))[0] if pc \
+        else qref.qparams_symmetric(wf.min(), wf.max())[0]
+    wq = qref.quantize_weight(wf, s_w)
+    b = (rng.standard_normal(cout) * 0.3).astype(F32)
+    s_x, s_y = F32(0.02), F32(0.3)
+    d = _layer(dev, wq, s_x, s_w, s_y, b, zx, zy, False, (2, 2), (0, 0))
+    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d, impl="gemm").cpu().numpy()
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, False, (2, 2), (0, 0))
+    assert out.shape == ref.shape
+    assert np.array_equal(out, ref)
+    assert len(np.unique(ref)) > 8, "degenerate case"
+
+
 def test_add_relu_golden_and_ragged(dev, golden_dir):
     from qconvnet import ops
     z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
