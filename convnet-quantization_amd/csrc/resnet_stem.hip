@@ -10,8 +10,8 @@
 // three-launch form — qcn_stem_pack_f32_nchw, the 7x1 conv_gemm over the
 // packed rows, qcn_maxpool3x3s2_u8_nhwc — moved ~1.6 GB per 512 images).
 //
-// One 512-thread workgroup per CU loops over bands of P = 2 pool rows of one
-// image.  A band needs CR = 2P + 1 conv rows (the conv row shared with the
+// One 512-thread workgroup per CU loops over bands of P = 4 (or 2) pool rows
+// of one image.  A band needs CR = 2P + 1 conv rows (the conv row shared with the
 // previous band is recomputed) and IR = 4P + 7 input rows.  Per band:
 //   A  the input rows are quantized (A1: q = clamp(zp + rint(x * inv), 0, 255))
 //      into QIN, 3 bytes per column (channel fastest), zero-point columns on
@@ -29,6 +29,8 @@
 // The next band's fp32 input is loaded into registers during C and D.
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
+
+#include <cstdlib>
 
 namespace qcn {
 
@@ -50,9 +52,9 @@ struct StemMax {
   }
 };
 
-template <int S>
+template <int S, int P_ = 2>
 struct StemCfg {
-  static constexpr int P = 2, CR = 2 * P + 1, IR = 4 * P + 7;
+  static constexpr int P = P_, CR = 2 * P + 1, IR = 4 * P + 7;
   static constexpr int OW = S / 2, PW = S / 4, C = 64;
   static constexpr int BANDS = PW / P;            // bands per image
   static constexpr int QL = 4;                    // zero-point columns left of a QIN row
@@ -87,9 +89,9 @@ struct StemArgs {
   uint8_t* y;
 };
 
-template <int S>
+template <int S, int P = 2>
 __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
-  using C = StemCfg<S>;
+  using C = StemCfg<S, P>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -280,17 +282,29 @@ __global__ __launch_bounds__(512, 1) void stem_fused_kernel(StemArgs a) {
 }  // namespace qcn
 
 namespace {
-template <int S>
+template <int S, int P = 2>
 int launch_stem(const qcn::StemArgs& a, hipStream_t st) {
-  using C = qcn::StemCfg<S>;
+  using C = qcn::StemCfg<S, P>;
   static bool attr_done[QCN_MAX_DEV] = {};
-  if (!qcn_set_lds_once((const void*)qcn::stem_fused_kernel<S>, C::LDS, attr_done)) return QCN_ERR_HIP;
+  if (!qcn_set_lds_once((const void*)qcn::stem_fused_kernel<S, P>, C::LDS, attr_done)) return QCN_ERR_HIP;
   const int ncu = qcn_cu_count();
   if (ncu <= 0) return QCN_ERR_HIP;
   const long nb = (long)a.n * C::BANDS;
   const int grid = (int)(nb < ncu ? nb : ncu);
-  hipLaunchKernelGGL(qcn::stem_fused_kernel<S>, dim3(grid), dim3(C::NTH), C::LDS, st, a);
+  hipLaunchKernelGGL((qcn::stem_fused_kernel<S, P>), dim3(grid), dim3(C::NTH), C::LDS, st, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+// Pool rows per band at 224² (QCN_STEM_P, an A/B switch): 4 by default — a
+// band of 9 conv rows recomputes one shared conv row per 8 instead of per 4
+// and passes its three barriers half as often per image: 0.422 -> 0.329 ms,
+// ResNet-50 106.2-108.2 -> 108.3-109.0 K img/s same box (1 pool row, two
+// workgroups per CU at 128 VGPRs, 0.549 ms; profiles/r03_diag_resnet_stem_band_ab.txt)
+int stem_band_rows() {
+  static const int p = [] {
+    const char* e = std::getenv("QCN_STEM_P");
+    return e && std::atoi(e) == 2 ? 2 : 4;
+  }();
+  return p;
 }
 }  // namespace
 
@@ -308,5 +322,6 @@ extern "C" int qcn_resnet_stem_fused(const float* x, int nimg, int h, int w, flo
   a.x = x; a.n = nimg; a.inv = 1.0f / in_scale; a.zp = in_zp; a.w = w_packed;
   a.u = u; a.v = v; a.mult = mult; a.corr = corr; a.zp_y = y_zp; a.lo = relu ? y_zp : 0; a.y = y;
   hipStream_t st = (hipStream_t)stream;
-  return h == 224 ? launch_stem<224>(a, st) : launch_stem<64>(a, st);
+  if (h == 64) return launch_stem<64>(a, st);
+  return stem_band_rows() == 2 ? launch_stem<224, 2>(a, st) : launch_stem<224, 4>(a, st);
 }
