@@ -78,8 +78,9 @@ KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel",
                              "convpair_ga_split_kernel"),
                   "conv3456": ("conv3456_kernel",),
+                  # the one-launch head (fc_head_kernel, default) or the two-launch form:
                   # "fc_finish" matches fc_finish_kernel (static) and fc_finish_qdq_kernel (QDQ)
-                  "fc12": ("fc_splitk_kernel", "fc_finish"),
+                  "fc12": ("fc_head_kernel", "fc_splitk_kernel", "fc_finish"),
                   "fc1": ("linear_u8s8_kernel",), "fc2": ("linear_f32_kernel",)}
 
 

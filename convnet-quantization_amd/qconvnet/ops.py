@@ -198,7 +198,9 @@ def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=F
 
 
 def classifier_workspace(m, n1, device):
-    return torch.empty(lib().qcn_classifier_workspace_size(m, n1), dtype=torch.uint8, device=device)
+    # zero-filled once: the one-launch head's arrival counters live at its end
+    # (each launch leaves them at zero again)
+    return torch.zeros(lib().qcn_classifier_workspace_size(m, n1), dtype=torch.uint8, device=device)
 
 
 def pack_fc_kmajor(w: np.ndarray):

@@ -189,14 +189,17 @@ int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, i
 /* A9 x 2 + A7 — the static classifier head in two launches: fc1 (+ReLU)
  * u8 x s8 -> u8 [m, n1] as a 4-way split-K GEMM into an int32 workspace, then
  * one wave per row finishes fc1 (requant) and computes fc2 (n2 <= 16) and its
- * DeQuantStub.  Same results as qcn_linear_u8s8(fc1) followed by
+ * DeQuantStub (env QCN_FC_FUSED=1: one launch whose last-arriving workgroups
+ * finish, through arrival counters in the workspace — slower, kept for A/B).  Same results as qcn_linear_u8s8(fc1) followed by
  * qcn_linear_u8s8(fc2, y_deq) — fc2's input zero point is y1_zp, fc2's
  * correction is applied exactly in the finisher (no corr2 argument).
  * x and w1 are CHUNK-MAJOR: x[k/32][m][32] (qcn_conv3x3_u8s8_kmajor writes
  * conv6's output that way), w1[k/32][n1][32] (qcn_pack_fc_kmajor).
  * corr1 = (128 - x_zp) * sum_k w1[f][k].  Supported: m % 128 == 0, n1 == 512,
- * k % 1024 == 0, n2 <= 16 (QCN_ERR_UNSUPPORTED otherwise).  workspace: device
- * memory of qcn_classifier_workspace_size(m, n1) bytes. */
+ * k % 1024 == 0, n2 <= 16, m <= 65536 (QCN_ERR_UNSUPPORTED otherwise).  workspace: device
+ * memory of qcn_classifier_workspace_size(m, n1) bytes, zero-filled before
+ * its first use (every launch leaves its counters at zero); one workspace per
+ * stream the head runs on concurrently. */
 long long qcn_classifier_workspace_size(int m, int n1);
 /* Host: s8 [n][k] row-major -> [k/32][n][32] (k % 32 == 0). */
 int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out);
