@@ -619,8 +619,12 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   constexpr int ROWB = NW * 32, RS = ROWB + 16, LPR = ROWB / 16, RPW = 64 / LPR;
   static_assert(RPW * NW == 32, "each wave moves 32 / NW rows of a strip");
   // B ring (BL): 1-KiB pieces of RPB pixel rows, CPR 16-B chunks per row
-  constexpr int CPR = K / 16, RPB = 1024 / K, NDMA = KC / NW, RING = BL ? P * 32 * K : 16;
-  static_assert(!BL || NDMA * NW == KC, "every wave loads the same number of B pieces");
+  // NDMA pieces per wave; with fewer pieces than waves (K = 64) the spare
+  // waves repeat a piece into a scratch slot, so every wave issues the same
+  // vector-memory ops (the vmcnt bounds are per wave)
+  constexpr int CPR = K / 16, RPB = 1024 / K, NDMA = (KC + NW - 1) / NW;
+  constexpr int RING = BL ? P * 32 * K + (NDMA * NW > KC ? 1024 : 0) : 16;
+  static_assert(!BL || NDMA * NW == KC || NDMA == 1, "pieces split evenly, or one per wave");
   __shared__ __attribute__((aligned(16))) uint8_t tile[2][32 * RS];
   __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
   const int rrow = wave * RPW + lane / LPR, rcol = (lane % LPR) * 16;
@@ -648,8 +652,9 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
       const int row = lane / CPR;   // row within the piece
 #pragma unroll
       for (int j = 0; j < NDMA; ++j) {
-        const int i = wave + NW * j, r = i * RPB + row;
-        glds16(a.x + (long)in_pix(pix(st, r)) * K + ((lane % CPR) ^ swz(r)) * 16, ring + q * 32 * K + i * 1024);
+        const int i = wave + NW * j, ip = i < KC ? i : i % KC, r = ip * RPB + row;
+        uint8_t* dst = i < KC ? ring + q * 32 * K + i * 1024 : ring + P * 32 * K;
+        glds16(a.x + (long)in_pix(pix(st, r)) * K + ((lane % CPR) ^ swz(r)) * 16, dst);
       }
     } else {
       const int xo = pix(st, l32) * K + hi * 16;
@@ -850,6 +855,10 @@ int dispatch_stream(GemmArgs& a, hipStream_t st) {
     const char* e = std::getenv("QCN_STREAM_BL128");
     return e ? std::atoi(e) != 0 : true;
   }();
+  static const bool bl64 = [] {   // A/B switch: K = 64 through the ring too
+    const char* e = std::getenv("QCN_STREAM_BL64");
+    return e && std::atoi(e) != 0;
+  }();
   // 32-bit buffer offsets
   if (a.npix * (long)(a.cin > a.cout ? a.cin : a.cout) >= (1L << 31) - 4096) return -1;
   if (a.cout % 128 != 0) {
@@ -862,7 +871,7 @@ int dispatch_stream(GemmArgs& a, hipStream_t st) {
     }
   }
   switch (a.cin) {
-    case 64: return stream_modes<64, 4, RESID, 4, false>(a, st);
+    case 64: return bl64 ? stream_modes<64, 4, RESID, 4, true>(a, st) : stream_modes<64, 4, RESID, 4, false>(a, st);
     case 128: return bl128 ? stream_modes<128, 4, RESID, 4, true>(a, st) : stream_modes<128, 4, RESID, 3, false>(a, st);
     case 256: return stream_modes<256, 4, RESID, 4, true>(a, st);
     case 512: return stream_modes<512, 4, RESID, 3, true>(a, st);
