@@ -837,6 +837,184 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
 // no streaming form.  Activations through the LDS ring for K >= 128 with 4
 // waves (QCN_STREAM_BL128=0: K = 128 into registers; the layer-2 expand convs
 // 0.126 -> 0.108 ms through the ring, profiles/r03_diag_resnet_stream_ab.txt).
+// ---------------------------------------------------------------------------
+// Whole-image 3x3 stride-1 conv for the small deep maps (layer 3: 14x14, 256
+// channels; layer 4: 7x7, 512): the implicit GEMM above gathers a 64-B im2col
+// row per output pixel and tap (nine per input byte), and at these shapes it
+// is bound by that gather (0.09-0.10 ms per conv at batch 512).  Here one
+// 8-wave workgroup takes one image and 256 output channels: the image is
+// staged once in LDS (q ^ 0x80, zero-point halo), wave w owns channel tile w
+// for ALL of the image's pixel tiles (NPT = ceil(HW^2 / 32), 7 or 2), its A
+// fragments stream from L2 into registers D K-steps ahead, and every tap of a
+// pixel tile is an immediate offset from the lane's patch address.  The patch
+// row stride is padded so a 16-lane ds_read_b128 group (16 consecutive
+// pixels) lands on 16 distinct 16-B bank slots across the row wraps.
+// Epilogue: FBGEMM requant (+ReLU floor), permlane swaps, an LDS [pixel][256]
+// tile and whole-row 16-B stores.
+template <int HW, int CIN, int NS = 1>
+struct ImgCfg {
+  static constexpr int COUT = 256;                   // channels per workgroup
+  // NS waves per channel tile, each taking JW of the image's pixel tiles
+  static constexpr int NW = 8 * NS, NT = NW * 64;
+  static constexpr int NPX = HW * HW, NPT = (NPX + 31) / 32, JW = (NPT + NS - 1) / NS;
+  static constexpr int KC = 9 * CIN / 32;            // K-steps (r, s, 32-channel chunk)
+  static constexpr int PW = HW + 2;
+  static constexpr int PS = CIN + 16;                // pixel stride: 1 slot (mod 16) per pixel
+  static constexpr int RS0 = PW * PS;
+  // row stride with (RS / 16) % 16 == HW % 16: slot(pixel) = pixel index mod 16
+  static constexpr int RS = RS0 + ((HW - RS0 / 16) % 16 + 16) % 16 * 16;
+  static constexpr int PATCH = PW * RS;
+  static constexpr int OS = COUT + 16;
+  static constexpr int OUT = NPX * OS;
+  static constexpr int LDS = (PATCH > OUT ? PATCH : OUT);
+  static_assert(PS % 256 == 16 && (RS / 16) % 16 == HW % 16, "conflict-free patch reads");
+  static_assert(CIN % 64 == 0, "whole 64-channel chunks");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int HW, int CIN, int D, int NS>
+__global__ __launch_bounds__((ImgCfg<HW, CIN, NS>::NT), 1) void conv3x3_img_kernel(GemmArgs a) {
+  using C = ImgCfg<HW, CIN, NS>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int ncg = a.cout / C::COUT;
+  const int img = blockIdx.x / ncg, cg = blockIdx.x % ncg;
+  const int ct = wave % 8, jg = wave / 8;             // channel tile, pixel-tile group
+  const int co0 = cg * C::COUT + ct * 32;            // this wave's channel tile
+
+  // ---- stage the image: 16-B pieces, q ^ 0x80; halo = zp ^ 0x80
+  const uint8_t* xi = a.x + (long)img * C::NPX * CIN;
+  constexpr int PPP = CIN / 16;                      // pieces per pixel
+  constexpr int NPC = C::NPX * PPP;
+  constexpr int PPT = (NPC + C::NT - 1) / C::NT;
+  uint4 pc[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int e = tid + C::NT * i;
+    pc[i] = e < NPC ? *reinterpret_cast<const uint4*>(xi + (long)e * 16) : make_uint4(0, 0, 0, 0);
+  }
+  // weights: A fragment of K-step kc for this wave's channel tile
+  const int8_t* wl = a.w + ((long)co0 + l32) * 32 + hi * 16;
+  const long wstep = (long)a.cout * 32;
+  v4i wq[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) wq[d] = *reinterpret_cast<const v4i*>(wl + d * wstep);
+  v16i corr;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int4 c4 = *reinterpret_cast<const int4*>(a.corr + co0 + 8 * g + 4 * hi);
+    corr[4 * g] = c4.x; corr[4 * g + 1] = c4.y; corr[4 * g + 2] = c4.z; corr[4 * g + 3] = c4.w;
+  }
+  const uint32_t zq = xor80(splat_u8(a.x_zp));
+  {
+    // halo pixels: rows 0 and HW+1, columns 0 and HW+1 of the patch
+    constexpr int NH = 2 * C::PW + 2 * HW;
+    for (int e = tid; e < NH * PPP; e += C::NT) {
+      const int hp = e / PPP, k = e % PPP;
+      int py, px;
+      if (hp < C::PW) { py = 0; px = hp; }
+      else if (hp < 2 * C::PW) { py = HW + 1; px = hp - C::PW; }
+      else { py = 1 + (hp - 2 * C::PW) / 2; px = (hp - 2 * C::PW) % 2 ? HW + 1 : 0; }
+      *reinterpret_cast<uint4*>(lds + py * C::RS + px * C::PS + 16 * k) = make_uint4(zq, zq, zq, zq);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int e = tid + C::NT * i;
+    if (e < NPC) {
+      const int p = e / PPP, k = e % PPP, y = p / HW, x = p % HW;
+      const uint4 v = pc[i];
+      *reinterpret_cast<uint4*>(lds + (y + 1) * C::RS + (x + 1) * C::PS + 16 * k) =
+          make_uint4(xor80(v.x), xor80(v.y), xor80(v.z), xor80(v.w));
+    }
+  }
+  __syncthreads();
+
+  // ---- main loop: lane (l32, hi) of pixel tile j reads pixel j*32 + l32
+  // (clamped; its outputs are never stored), channels 16 hi of the chunk
+  int pb[C::JW];
+#pragma unroll
+  for (int j = 0; j < C::JW; ++j) {
+    int p = (jg * C::JW + j) * 32 + l32;
+    p = p < C::NPX ? p : C::NPX - 1;
+    pb[j] = (p / HW) * C::RS + (p % HW) * C::PS + hi * 16;
+  }
+  v16i acc[C::JW];
+#pragma unroll
+  for (int kc = 0; kc < C::KC; ++kc) {
+    const int tap = kc / (CIN / 32), ch = kc % (CIN / 32);
+    const int off = (tap / 3) * C::RS + (tap % 3) * C::PS + ch * 32;
+    const v4i wa = wq[kc % D];
+    if (kc + D < C::KC) wq[kc % D] = *reinterpret_cast<const v4i*>(wl + (kc + D) * wstep);
+#pragma unroll
+    for (int j = 0; j < C::JW; ++j) {
+      const v4i b = *reinterpret_cast<const v4i*>(lds + pb[j] + off);
+      acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wa, b, kc == 0 ? corr : acc[j], 0, 0, 0);
+    }
+  }
+  __syncthreads();   // the patch is dead: its space becomes the output tile
+
+  // ---- epilogue: requant (+ReLU floor) -> bytes -> 16 consecutive channels
+  // per lane -> LDS [pixel][OS] -> whole-row stores
+  {
+    float u[16], v[16], m[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int co = co0 + 8 * g + 4 * hi;
+      const float4 x4 = *reinterpret_cast<const float4*>(a.u + co);
+      const float4 y4 = *reinterpret_cast<const float4*>(a.v + co);
+      const float4 z4 = *reinterpret_cast<const float4*>(a.mult + co);
+      u[4 * g] = x4.x; u[4 * g + 1] = x4.y; u[4 * g + 2] = x4.z; u[4 * g + 3] = x4.w;
+      v[4 * g] = y4.x; v[4 * g + 1] = y4.y; v[4 * g + 2] = y4.z; v[4 * g + 3] = y4.w;
+      m[4 * g] = z4.x; m[4 * g + 1] = z4.y; m[4 * g + 2] = z4.z; m[4 * g + 3] = z4.w;
+    }
+    const float zpf = (float)a.zp_y, lof = (float)a.lo;
+#pragma unroll
+    for (int j = 0; j < C::JW; ++j) {
+      uint32_t w[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(requant_f(acc[j][r], u[r], v[r], m[r], zpf, lof), e, wd);
+        }
+        w[g] = wd;
+      }
+      auto s01 = __builtin_amdgcn_permlane32_swap(w[0], w[1], false, false);
+      auto s23 = __builtin_amdgcn_permlane32_swap(w[2], w[3], false, false);
+      w[0] = s01[0]; w[1] = s01[1]; w[2] = s23[0]; w[3] = s23[1];
+      auto s02 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+      auto s13 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+      w[0] = s02[0]; w[2] = s02[1]; w[1] = s13[0]; w[3] = s13[1];
+      const int p = (jg * C::JW + j) * 32 + l32;
+      if (p < C::NPX)
+        *reinterpret_cast<uint4*>(lds + p * C::OS + ct * 32 + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  __syncthreads();
+  constexpr int TPR = C::COUT / 16;                  // threads per pixel row
+  uint8_t* yo = a.y + (long)img * C::NPX * a.cout + cg * C::COUT;
+  for (int e = tid; e < C::NPX * TPR; e += C::NT) {
+    const int p = e / TPR, k = e % TPR;
+    *reinterpret_cast<uint4*>(yo + (long)p * a.cout + 16 * k) =
+        *reinterpret_cast<const uint4*>(lds + p * C::OS + 16 * k);
+  }
+}
+
+template <int HW, int CIN, int D, int NS>
+int launch_img(GemmArgs& a, hipStream_t st) {
+  using C = ImgCfg<HW, CIN, NS>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)conv3x3_img_kernel<HW, CIN, D, NS>, C::LDS, attr_done)) return QCN_ERR_HIP;
+  hipLaunchKernelGGL((conv3x3_img_kernel<HW, CIN, D, NS>), dim3(a.n * (a.cout / C::COUT)), dim3(C::NT), C::LDS, st,
+                     a);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 // the stride-2 downsample 1x1 (no padding, K in {256, 512}, Cout % 128 == 0)
 inline int dispatch_stream_s2(GemmArgs& a, hipStream_t st) {
   if (a.npix * (long)a.cout >= (1L << 31) - 4096 || (long)a.n * a.h * a.w_ * a.cin >= (1L << 31) - 4096 ||
@@ -925,6 +1103,21 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   if (cin <= stream_k && kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && pad_h == 0 && pad_w == 0) {
     const int rc = resid ? qcn::dispatch_stream<true>(a, st) : qcn::dispatch_stream<false>(a, st);
     if (rc >= 0) return rc;
+  }
+  // whole-image 3x3 for the 14x14x256 and 7x7x512 maps (QCN_GEMM_IMG3=0: tiled)
+  // (1 = 8 waves per image, 2 = 16 waves: two per channel tile; 3 = also the
+  // 7x7x512 maps).  Same box: layer-3 3x3 0.105 -> 0.090 ms at 16 waves
+  // (0.092 at 8); the 7x7x512 convs 0.095 -> 0.110 ms, so they stay tiled
+  // (profiles/r03_diag_resnet_img3_ab.txt)
+  static const int img3 = [] {
+    const char* e = std::getenv("QCN_GEMM_IMG3");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (img3 && !resid && kh == 3 && kw == 3 && stride_h == 1 && stride_w == 1 && pad_h == 1 && pad_w == 1 &&
+      h == w && cout % 256 == 0) {
+    if (h == 14 && cin == 256)
+      return img3 == 1 ? qcn::launch_img<14, 256, 4, 1>(a, st) : qcn::launch_img<14, 256, 8, 2>(a, st);
+    if (h == 7 && cin == 512 && img3 == 3) return qcn::launch_img<7, 512, 8, 2>(a, st);
   }
   // the stride-2 downsample 1x1 streams too (QCN_GEMM_STREAM_S2=0: tiled)
   static const bool stream_s2 = [] {

@@ -209,6 +209,37 @@ def test_conv1x1_stride2_stream_oracle(dev, shape):
     assert len(np.unique(ref)) > 8, "degenerate case"
 
 
+@pytest.mark.parametrize("shape", [
+    # n, hw, cin, cout, zx, relu, zy, per_channel
+    (2, 14, 256, 256, 7, True, 0, True),
+    (1, 14, 256, 512, 200, False, 40, False),   # two 256-channel groups per image
+    (3, 7, 512, 512, 0, True, 9, True),         # ReLU floor at zy > 0
+    (1, 7, 512, 256, 131, False, 0, False),
+])
+def test_conv3x3_whole_image_oracle(dev, shape):
+    """The whole-image 3x3 kernel (conv3x3_img_kernel: the layer-3 14x14x256
+    maps, one image x 256 channels per workgroup; the 7x7x512 shapes run it
+    with QCN_GEMM_IMG3=3, the tiled kernel by default) against the oracle's
+    conv, per-channel and per-tensor."""
+    from qconvnet import ops
+    n, hw, cin, cout, zx, relu, zy, pc = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, hw, hw, cin)).astype(np.uint8)
+    wf = (rng.standard_normal((cout, cin, 3, 3)) * 0.02).astype(F32)
+    s_w = qref.qparams_symmetric(wf.reshape(cout, -1).min(1), wf.reshape(cout, -1).max(1))[0] if pc \
+        else qref.qparams_symmetric(wf.min(), wf.max())[0]
+    wq = qref.quantize_weight(wf, s_w)
+    b = (rng.standard_normal(cout) * 0.3).astype(F32)
+    s_x, s_y = F32(0.02), F32(0.6)
+    d = _layer(dev, wq, s_x, s_w, s_y, b, zx, zy, relu, (1, 1), (1, 1))
+    out = ops.conv(torch.from_numpy(qx).to(dev), zx, d, impl="gemm").cpu().numpy()
+    u, v, mult = qref.requant_constants(s_x, s_w, s_y, b)
+    ref = qref.conv_q(qx, zx, wq, u, v, mult, zy, relu, (1, 1), (1, 1))
+    assert out.shape == ref.shape
+    assert np.array_equal(out, ref)
+    assert len(np.unique(ref)) > 8, "degenerate case"
+
+
 def test_add_relu_golden_and_ragged(dev, golden_dir):
     from qconvnet import ops
     z = dict(np.load(os.path.join(golden_dir, "ops_resnet.npz")))
