@@ -841,7 +841,8 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
 // Whole-image 3x3 stride-1 conv for the small deep maps (layer 3: 14x14, 256
 // channels; layer 4: 7x7, 512): the implicit GEMM above gathers a 64-B im2col
 // row per output pixel and tap (nine per input byte), and at these shapes it
-// is bound by that gather (0.09-0.10 ms per conv at batch 512).  Here one
+// is bound by that gather (0.09-0.10 ms per conv at batch 512; 0.065 / 0.073
+// ms here).  Here one
 // 8-wave workgroup takes one image and 256 output channels: the image is
 // staged once in LDS (q ^ 0x80, zero-point halo), wave w owns channel tile w
 // for ALL of the image's pixel tiles (NPT = ceil(HW^2 / 32), 7 or 2), its A
@@ -942,17 +943,31 @@ __global__ __launch_bounds__((ImgCfg<HW, CIN, NS>::NT), 1) void conv3x3_img_kern
     pb[j] = (p / HW) * C::RS + (p % HW) * C::PS + hi * 16;
   }
   v16i acc[C::JW];
+  // software pipeline (sched_barrier fences keep it: left alone, the
+  // scheduler sank every load next to its use, one vmcnt(0) / lgkmcnt(0) per
+  // MFMA): the next K-step's B fragments are read during this step's MFMAs,
+  // and the A fragment D steps ahead is loaded right after this step's use
+  auto koff = [](int kc) {
+    const int tap = kc / (CIN / 32), ch = kc % (CIN / 32);
+    return (tap / 3) * C::RS + (tap % 3) * C::PS + ch * 32;
+  };
+  v4i bb[2][C::JW];
+#pragma unroll
+  for (int j = 0; j < C::JW; ++j) bb[0][j] = *reinterpret_cast<const v4i*>(lds + pb[j] + koff(0));
 #pragma unroll
   for (int kc = 0; kc < C::KC; ++kc) {
-    const int tap = kc / (CIN / 32), ch = kc % (CIN / 32);
-    const int off = (tap / 3) * C::RS + (tap % 3) * C::PS + ch * 32;
-    const v4i wa = wq[kc % D];
-    if (kc + D < C::KC) wq[kc % D] = *reinterpret_cast<const v4i*>(wl + (kc + D) * wstep);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kc + 1 < C::KC) {
 #pragma unroll
-    for (int j = 0; j < C::JW; ++j) {
-      const v4i b = *reinterpret_cast<const v4i*>(lds + pb[j] + off);
-      acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wa, b, kc == 0 ? corr : acc[j], 0, 0, 0);
+      for (int j = 0; j < C::JW; ++j)
+        bb[(kc + 1) & 1][j] = *reinterpret_cast<const v4i*>(lds + pb[j] + koff(kc + 1));
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < C::JW; ++j)
+      acc[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(wq[kc % D], bb[kc & 1][j], kc == 0 ? corr : acc[j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kc + D < C::KC) wq[kc % D] = *reinterpret_cast<const v4i*>(wl + (kc + D) * wstep);
   }
   __syncthreads();   // the patch is dead: its space becomes the output tile
 
@@ -1105,9 +1120,9 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
     if (rc >= 0) return rc;
   }
   // whole-image 3x3 for the 14x14x256 and 7x7x512 maps (QCN_GEMM_IMG3=0: tiled)
-  // (1 = 8 waves per image, 2 = 16 waves: two per channel tile; 3 = also the
-  // 7x7x512 maps).  Same box: layer-3 3x3 0.105 -> 0.090 ms at 16 waves
-  // (0.092 at 8); the 7x7x512 convs 0.095 -> 0.110 ms, so they stay tiled
+  // (QCN_GEMM_IMG3: 0 = tiled, 1 = the 14x14x256 maps only, 2 = also the
+  // 7x7x512 maps).  Same box: layer-3 3x3 0.101 -> 0.065 ms, layer-4 0.094 ->
+  // 0.073 ms, ResNet-50 108.6-109.3 -> 114.5-114.6 K img/s
   // (profiles/r03_diag_resnet_img3_ab.txt)
   static const int img3 = [] {
     const char* e = std::getenv("QCN_GEMM_IMG3");
@@ -1115,9 +1130,8 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   }();
   if (img3 && !resid && kh == 3 && kw == 3 && stride_h == 1 && stride_w == 1 && pad_h == 1 && pad_w == 1 &&
       h == w && cout % 256 == 0) {
-    if (h == 14 && cin == 256)
-      return img3 == 1 ? qcn::launch_img<14, 256, 4, 1>(a, st) : qcn::launch_img<14, 256, 8, 2>(a, st);
-    if (h == 7 && cin == 512 && img3 == 3) return qcn::launch_img<7, 512, 8, 2>(a, st);
+    if (h == 14 && cin == 256) return qcn::launch_img<14, 256, 8, 1>(a, st);
+    if (h == 7 && cin == 512 && img3 == 2) return qcn::launch_img<7, 512, 8, 1>(a, st);
   }
   // the stride-2 downsample 1x1 streams too (QCN_GEMM_STREAM_S2=0: tiled)
   static const bool stream_s2 = [] {

@@ -218,9 +218,8 @@ def test_conv1x1_stride2_stream_oracle(dev, shape):
 ])
 def test_conv3x3_whole_image_oracle(dev, shape):
     """The whole-image 3x3 kernel (conv3x3_img_kernel: the layer-3 14x14x256
-    maps, one image x 256 channels per workgroup; the 7x7x512 shapes run it
-    with QCN_GEMM_IMG3=3, the tiled kernel by default) against the oracle's
-    conv, per-channel and per-tensor."""
+    and layer-4 7x7x512 maps, one image x 256 channels per 8-wave workgroup)
+    against the oracle's conv, per-channel and per-tensor."""
     from qconvnet import ops
     n, hw, cin, cout, zx, relu, zy, pc = shape
     rng = np.random.default_rng(hash(shape) & 0xffff)

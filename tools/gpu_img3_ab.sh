@@ -1,5 +1,5 @@
 # r03: whole-image 3x3 kernel for the 14x14x256 / 7x7x512 maps (QCN_GEMM_IMG3
-# 0 = tiled, 1 = 8 waves per image, 2 = 16): tests, same-box config-5 bench
+# 0 = tiled, 1 = 14x14 maps, 2 = also 7x7x512): tests, same-box config-5 bench
 # A/B and per-layer times.
 set -e
 cd $GRAFT_REPO_ROOT
@@ -7,7 +7,7 @@ O=gpurun_out/r03_img3
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_resnet.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
 tail -1 $O/t.log
-QCN_GEMM_IMG3=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_resnet.py -m gpu -x -q --timeout 200 --timeout-method thread -k "whole_image or bit_exact" > $O/t1.log 2>&1 || { tail -40 $O/t1.log; exit 1; }
+QCN_GEMM_IMG3=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_resnet.py -m gpu -x -q --timeout 200 --timeout-method thread -k "whole_image or bit_exact" > $O/t1.log 2>&1 || { tail -40 $O/t1.log; exit 1; }
 tail -1 $O/t1.log
 for V in 0 1 2 0 1 2; do
   QCN_GEMM_IMG3=$V timeout -k 10 300 python bench.py --workload resnet50 --steps 20 --warmup 5 --no-cpu --no-pmc 2>/dev/null | python -c "
