@@ -128,6 +128,41 @@ def load_payload(path):
     return _dec(torch.load(path, weights_only=True))
 
 
+WARMUP_MIN_S = 0.1   # untimed forwards after the W warmup steps, at least this long
+
+
+def ramp_warmup(step, drain, warmup, world, dev, min_s=WARMUP_MIN_S):
+    """The W warmup steps, then more untimed steps until at least min_s of
+    back-to-back forwards have run.  After an idle spell the chip needs a few
+    ms of load to reach the throughput it then holds: on one box the headline
+    read 6.2-6.5 M img/s after 10 warmup steps and 7.1-7.2 M after 200 (or
+    over 300-1000 timed steps), profiles/r03_diag_warmup.txt.  The extra step
+    count comes from a 5-step probe and is the max over ranks, so every rank
+    runs the same number of steps (their logits all-gathers pair up).
+    Returns the number of warmup steps run."""
+    for _ in range(warmup):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    per = (time.perf_counter() - t0) / 5
+    extra = max(0, int(np.ceil(min_s / max(per, 1e-6))) - warmup - 5)
+    if world > 1:
+        tdev = dev if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([extra], dtype=torch.int64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra = int(t.item())
+    for _ in range(extra):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    return warmup + 5 + extra
+
+
 def under_profiler():
     """True when this process already runs under rocprofv3 (its preloaded tool
     library initialised the GPU before main): a nested rocprofv3 child would then
@@ -312,7 +347,7 @@ def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static"):
     out = tempfile.mkdtemp(prefix="qcn_pmc_", dir="/tmp")
     cmd = [exe, "--pmc", *counters, "--kernel-include-regex", "qcn::", "-f", "csv", "-d", out,
            "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup",
-           "1", "--no-cpu", "--no-pmc", "--batch", str(batch), "--spec-file", spec_file]
+           "1", "--warmup-min-ms", "0", "--no-cpu", "--no-pmc", "--batch", str(batch), "--spec-file", spec_file]
     if per_channel:
         cmd.append("--per-channel")
     if mode != "static":
@@ -433,6 +468,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup-min-ms", type=float, default=WARMUP_MIN_S * 1e3,
+                    help="after the W warmup steps, keep running untimed forwards until this many ms "
+                         "of them have run (0: exactly W); see ramp_warmup()")
     ap.add_argument("--batch", type=int, default=None,
                     help="images per GPU (default 1024; 256 for --workload qdq, 512 for resnet50)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -513,10 +551,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
+    warm_run = ramp_warmup(step, drain, args.warmup, world, dev, args.warmup_min_ms * 1e-3)
 
     # ---- timed region A: the metric
     barrier()
@@ -642,7 +677,7 @@ def main():
 
     result = {
         "metric": METRIC if mode == "static" else METRIC_QDQ, "value": value, "unit": "images/sec", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup,
+        "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": warm_run,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int8", "data": "synthetic", "hip_graph": bool(use_graph),
         "config": {"workload": ("full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
@@ -749,9 +784,7 @@ def main_resnet(args):
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    warm_run = ramp_warmup(step, lambda: None, args.warmup, world, dev, args.warmup_min_ms * 1e-3)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -799,7 +832,8 @@ def main_resnet(args):
                     "HIP-event conv time; stem MACs counted at the packed K=224 actually issued"}
     result = {
         "metric": METRIC_RESNET, "value": value, "unit": "images/sec", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": warm_run,
+        "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic",
         "config": {"workload": "ResNet-50 (stem, 16 bottleneck blocks, avgpool, fc) static int8, "
