@@ -441,7 +441,7 @@ def pmc_counters(model, sd, args, names, timeout=150):
                     res[n]["sq_insts_valu"] = _per_launch(agg, n, "SQ_INSTS_VALU")
                     if busy is not None and gui:
                         # per SIMD: busy cycles / (1024 SIMDs x dispatch cycles per XCD)
-                        res[n]["mfma_busy"] = busy / (1024.0 * gui / 8.0)
+                        res[n]["mfma_busy_gui"] = busy / (1024.0 * gui / 8.0)
                     if v is None:
                         errors.append(f"{tag}: no counter row matched launch {n}")
         try:
@@ -659,13 +659,24 @@ def main():
         pmc, pmc_err = pmc_counters(model, sd, args, names)
         for n in names:
             kern[n].update({kk: vv for kk, vv in pmc[n].items() if vv is not None})
-        p = pmc[dom]
+            kn = kern[n]
+            if kn.get("sq_valu_mfma_busy_cycles") and kn.get("clock_ghz") and kn.get("ms"):
+                # issued MFMA cycles per SIMD over the launch's own SIMD cycles at the
+                # clock the chip holds in it (GRBM_GUI_ACTIVE / 8 reads high on
+                # dispatches this short, so mfma_busy_gui under-reads); equals
+                # frac * 2.4 / clock when a kernel issues exactly its algorithmic MFMAs
+                kn["mfma_busy"] = kn["sq_valu_mfma_busy_cycles"] / (1024.0 * kn["clock_ghz"] * 1e6 * kn["ms"])
+        p = kern[dom]
         roof["traffic"] = p.get("traffic_bytes")
         roof["traffic_note"] = ("HBM bytes per launch from rocprofv3 --pmc passes of a child run "
                                 "(same model, batch): 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); "
                                 f"algorithmic bytes per launch {BYTES_PER_IMAGE[dom] * B}")
         if p.get("mfma_busy") is not None:
             roof["mfma_busy"] = p["mfma_busy"]
+            roof["mfma_busy_note"] = ("SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x in-kernel clock x mean "
+                                      "HIP-event duration); counts issued MFMAs (32 cycles each), so it "
+                                      "exceeds mfma_issue_at_clock where a kernel recomputes (config 2's "
+                                      "split conv5+6 issues conv5 twice: 4/3)")
         if p.get("clock_ghz"):
             # the clock the chip holds in this kernel (in-kernel s_memtime /
             # s_memrealtime of a stamped diagnostic copy after >= 2 s of back-to-back
