@@ -53,7 +53,6 @@ MAC_PER_IMAGE["conv12"] = MAC_PER_IMAGE["conv1"] + MAC_PER_IMAGE["conv2"]
 MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
 MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
 MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
-MAC_PER_IMAGE["conv3456"] = MAC_PER_IMAGE["conv34"] + MAC_PER_IMAGE["conv56"]
 MAC_PER_IMAGE["net"] = sum(MAC_PER_IMAGE[f"conv{i}"] for i in range(1, 7))
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
@@ -67,20 +66,16 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "fc12": 4096 + 512 + 10 + 40,
                  "conv34": 16 * 16 * 64 + 8 * 8 * 128,
                  "conv56": 8 * 8 * 128 + 4 * 4 * 256,
-                 # a2 in, a4 out (read back from L2 inside the launch), a6 out
-                 "conv3456": 16 * 16 * 64 + 8 * 8 * 128 + 4 * 4 * 256,
                  "net": 3 * 32 * 32 * 4 + 4 * 4 * 256}
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
                   "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
                   # (one form runs per batch size: the split form at <= 1 image per CU)
-                  "conv56": ("convpair_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel",
-                             "convpair_ga_split_kernel"),
-                  "conv3456": ("conv3456_kernel",),
-                  # the one-launch head (fc_head_kernel, default) or the two-launch form:
-                  # "fc_finish" matches fc_finish_kernel (static) and fc_finish_qdq_kernel (QDQ)
-                  "fc12": ("fc_head_kernel", "fc_splitk_kernel", "fc_finish"),
+                  "conv56": ("convpair_ga_kernel", "convpair_ga_split_kernel"),
+                  # the two-launch head: "fc_finish" matches fc_finish_kernel (static)
+                  # and fc_finish_qdq_kernel (QDQ)
+                  "fc12": ("fc_splitk_kernel", "fc_finish"),
                   "fc1": ("linear_u8s8_kernel",), "fc2": ("linear_f32_kernel",)}
 
 
@@ -221,11 +216,26 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
         iters = max(20, int(seconds * probe / bs))
         thr = harness.measure_throughput(sp, batch_size=bs, num_iterations=iters, verbose=False)
     out["static_ptq"] = {"value": thr, "unit": "images/sec", "cores": threads,
-                         "kind": "port",
+                         "cpu_count": os.cpu_count(), "kind": "port",
                          "sample": f"BASELINE configs[0]: reference StaticPTQModel path (torch.ao "
                                    f"quantize_dynamic {{Linear,Conv2d}} qint8 on our SimpleConvNet "
                                    f"restatement), batch {bs} x {iters} iters through "
                                    f"utils.inference_benchmark.InferenceBenchmark.measure_throughput"}
+    # (1b) the same harness at the GPU batch sizes BASELINE.md §4 names (256,
+    #      1024), a third of the budget each
+    out["static_ptq_batches"] = {}
+    for bsb in (256, 1024):
+        xb = torch.from_numpy(data.synthetic_images(bsb, 13))
+        hb = InferenceBenchmark([(xb, torch.zeros(bsb, dtype=torch.long))], device="cpu")
+        with contextlib.redirect_stdout(sys.stderr):
+            hb.warm_up(sp, num_iterations=1)
+            pr = hb.measure_throughput(sp, batch_size=bsb, num_iterations=2, verbose=False)
+            it_b = max(2, int(seconds / 3 * pr / bsb))
+            tb = hb.measure_throughput(sp, batch_size=bsb, num_iterations=it_b, verbose=False)
+        out["static_ptq_batches"][str(bsb)] = {
+            "value": tb, "unit": "images/sec", "cores": threads, "cpu_count": os.cpu_count(),
+            "sample": f"reference StaticPTQModel path, batch {bsb} x {it_b} iters through "
+                      f"InferenceBenchmark.measure_throughput"}
     # (2) full static int8 on the CPU (torch.ao eager, fbgemm) — apples to apples
     calib = torch.from_numpy(data.synthetic_task(512, 1)[0])   # the GPU model's calibration set
     q = torch_ref.build_static_int8_cpu(fp, [calib])
@@ -240,7 +250,7 @@ def cpu_baselines(state_dict, qmodel_gpu, seconds):
             total += time.time() - t0
             iters += 1
     out["static_int8"] = {"value": bs2 * iters / total, "unit": "images/sec", "cores": threads,
-                          "kind": "port",
+                          "cpu_count": os.cpu_count(), "kind": "port",
                           "sample": f"torch.ao eager static int8 (fbgemm), batch {bs2} x {iters} iters"}
     # (3) top-1 on a held-out synthetic test set with true labels (the fp32
     #     model was trained on the same task; CIFAR-10 is not available offline)
@@ -301,7 +311,7 @@ def cpu_baseline_qdq(state_dict, qmodel_gpu, seconds):
             total += time.time() - t0
             iters += 1
     out = {"static_ptq": {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
-                          "kind": "port",
+                          "cpu_count": os.cpu_count(), "kind": "port",
                           "sample": f"BASELINE configs[1] on the CPU: per-layer QDQ SimpleConvNet "
                                     f"(torch.ao fbgemm, stubs converted), batch {bs} x {iters} iters"}}
     xe_np, ye_np = data.synthetic_task(4096, 77)
@@ -576,6 +586,34 @@ def main():
     images = world * B * args.steps
     value = images / elapsed
 
+    # ---- region S: sustained throughput, >= 1 s of back-to-back steps (a
+    # field beside the metric, never the metric: `value` is the K-step region)
+    per_step = elapsed / max(1, args.steps)
+    n_sus = max(args.steps, int(np.ceil(1.0 / max(per_step, 1e-6))))
+    if world > 1:
+        tdev = dev if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([n_sus], dtype=torch.int64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_sus = int(t.item())
+    barrier()
+    torch.cuda.synchronize()
+    t0s = time.perf_counter()
+    for _ in range(n_sus):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    barrier()
+    el_s = time.perf_counter() - t0s
+    if world > 1:
+        tdev = dev if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([el_s], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_s = float(t.item())
+    sustained = {"value": world * B * n_sus / el_s, "steps": n_sus, "seconds": el_s,
+                 "ms_per_step": el_s / n_sus * 1e3,
+                 "note": "the same step back to back for >= 1 s right after the timed region; "
+                         "reported beside the metric, not as it"}
+
     # ---- optional region C: batches in flight on several streams (serving)
     pipelined = None
     if args.pipeline > 1 and world == 1:
@@ -689,8 +727,12 @@ def main():
     result = {
         "metric": METRIC if mode == "static" else METRIC_QDQ, "value": value, "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": warm_run,
+        "warmup_note": (f"the W warmup steps, then untimed steps until >= {args.warmup_min_ms:.0f} ms of "
+                        "back-to-back forwards have run (ramp_warmup; --warmup-min-ms 0 runs exactly W), "
+                        "so the timed region starts at the throughput the chip holds under load"),
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int8", "data": "synthetic", "hip_graph": bool(use_graph),
+        "sustained": sustained,
         "config": {"workload": ("full static-PTQ SimpleConvNet, all conv+linear int8 (u8 x s8 -> i32), "
                                 "NHWC, per-tensor weights" if mode == "static" else
                                 "per-layer QDQ SimpleConvNet (CustomQuantizationModel, BASELINE configs[1]): "
@@ -711,6 +753,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baselines(sd, model, args.cpu_seconds)
         result["cpu_baseline"] = cb["static_ptq"]
+        if "static_ptq_batches" in cb:
+            result["cpu_static_ptq_batches"] = cb["static_ptq_batches"]
         if "static_int8" in cb:
             result["cpu_static_int8"] = cb["static_int8"]
         result["top1"] = cb["top1"]
@@ -753,7 +797,7 @@ def resnet_cpu_baseline(model_fp, seconds):
                 total += time.time() - t0
                 iters += 1
         out[name] = {"value": bs * iters / total, "unit": "images/sec", "cores": threads,
-                     "kind": "port", "sample": f"batch {bs} x {iters} iters"}
+                     "cpu_count": os.cpu_count(), "kind": "port", "sample": f"batch {bs} x {iters} iters"}
     out["static_int8"]["sample"] = ("torch.ao FX static int8 (fbgemm, per-channel) of the same "
                                     "ResNet-50, " + out["static_int8"]["sample"])
     out["fp32"]["sample"] = ("fp32 ResNet-50 (what CustomQuantizedResNet50 runs: its stubs are "

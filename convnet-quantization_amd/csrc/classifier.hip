@@ -23,19 +23,12 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
-#include <cstdlib>
-
 namespace qcn {
 
 constexpr int FC_S = 4;      // K split
 constexpr int FC_N1 = 512;   // fc1 features handled by the finisher (64 lanes x 8)
 constexpr int FC_N2 = 16;    // max fc2 outputs
-// workspace: arrival counters first, at fixed offsets for every batch size
-// (a workspace is reused across batch sizes; each launch leaves its counters
-// at zero), then the split-K partials and the fc2 partial sums
-constexpr int FC_MAXM = 65536;                    // rows supported
-constexpr int FC_MAXMB = FC_MAXM / 64;            // row blocks of >= 64 rows
-constexpr int FC_CNT = FC_MAXMB * (FC_N1 / 64) + FC_MAXMB;   // ints
+// workspace: the split-K partials, [FC_S][m][n1] int32
 
 // X' [K/32][m][32], W' [K/32][n][32] (chunk-major: a 32-row MFMA fragment of
 // one 32-byte K chunk is one contiguous 1 KB, every wave-load fully coalesced).
@@ -44,10 +37,8 @@ constexpr int FC_CNT = FC_MAXMB * (FC_N1 / 64) + FC_MAXMB;   // ints
 // traffic, for batches too small to fill the CUs with 128-row tiles).
 // fc1's split-K partial tile of workgroup blockIdx.x; returns its (row
 // block, feature block, K quarter)
-// COH: agent-coherent (sc1) stores, for a consumer on another XCD in the
-// same launch (the one-launch head)
-template <int RW, bool COH = false>
-QCN_DEV int3 fc_splitk_tile(const uint8_t* __restrict__ x, int m, int k, const int8_t* __restrict__ w, int n,
+template <int RW>
+QCN_DEV void fc_splitk_tile(const uint8_t* __restrict__ x, int m, int k, const int8_t* __restrict__ w, int n,
                             int* __restrict__ part) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int MB = m / (2 * RW), NB = n / 64, T = MB * NB * FC_S;
@@ -118,19 +109,6 @@ QCN_DEV int3 fc_splitk_tile(const uint8_t* __restrict__ x, int m, int k, const i
   // with the finisher, profiles/r02_diag_write_through_ab.txt)
   int* pp = part + (long)s * m * n + col0 + 4 * hi;
   const int r = row0 + l32;
-  if constexpr (COH) {
-    const wt_rsrc_t pr = wt_rsrc(part);
-    const uint32_t b0 = (uint32_t)(((long)s * m * n + col0 + 4 * hi) * 4);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      store_wt16(pr, b0 + (uint32_t)(((long)r * n + 8 * g) * 4),
-                 make_uint4(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]));
-      if constexpr (RW == 64)
-        store_wt16(pr, b0 + (uint32_t)(((long)(r + 32) * n + 8 * g) * 4),
-                   make_uint4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]));
-    }
-    return make_int3(mb, nb, s);
-  }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     *reinterpret_cast<int4*>(pp + (long)r * n + 8 * g) =
@@ -139,7 +117,6 @@ QCN_DEV int3 fc_splitk_tile(const uint8_t* __restrict__ x, int m, int k, const i
       *reinterpret_cast<int4*>(pp + (long)(r + 32) * n + 8 * g) =
           make_int4(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
   }
-  return make_int3(mb, nb, s);
 }
 
 template <int RW>
@@ -356,229 +333,6 @@ __global__ __launch_bounds__(256) void fc_finish_qdq_kernel(const int* __restric
   if (lane < hd.n2) y2f[(long)row * hd.n2 + lane] = mine + (hd.b2 ? hd.b2[lane] : 0.f);
 }
 
-// ---------------------------------------------------------------------------
-// The head in ONE launch: fc_splitk_tile, then the last of the FC_S K-quarter
-// workgroups of each (row block, feature block) tile finishes that tile — sums
-// the four partials, requantizes fc1 (y1) and computes fc2's partial sums over
-// the tile's 64 features — and the last of the NB tile finishers of a row
-// block finishes fc2 for its rows.  "Last" comes from per-tile and per-row-
-// block arrival counters in the workspace (a vector atomic after an
-// agent-scope release; the last arriver acquires and resets the counter, so
-// the workspace is ready for the next launch — it must be zero-filled once
-// before first use).  Nothing waits on another workgroup: every workgroup
-// either finishes work or leaves.  Removes the finisher launch, its ramp and
-// one dependent-launch boundary (measured slower, so not the default: see
-// fc_fused below).  fc2 in the integer head is exact sums
-// (bit-identical to fc_finish_kernel); the QDQ head's fp32 fc2 sums 16-32
-// features per lane, then lanes, then the 8 feature blocks in order.
-template <int RW, bool QDQ, class Head>
-__global__ __launch_bounds__(256) void fc_head_kernel(const uint8_t* __restrict__ x, int m, int k,
-                                                      const int8_t* __restrict__ w, int n, int* ws, Head hd,
-                                                      uint8_t* __restrict__ y1, uint8_t* __restrict__ y2,
-                                                      float* __restrict__ y2f) {
-  const int NB = n / 64;
-  int* cnt = ws;                                   // [FC_MAXMB][NB] tile arrivals
-  int* cnt2 = ws + FC_MAXMB * (FC_N1 / 64);        // [FC_MAXMB] row-block arrivals
-  int* part = ws + FC_CNT;
-  int* f2p = part + (long)FC_S * m * n;           // [NB][m][FC_N2] (int, or fp32 for QDQ)
-  const int3 t3 = fc_splitk_tile<RW, true>(x, m, k, w, n, part);
-  const int mb = t3.x, nb = t3.y;
-  const int tid = threadIdx.x, lane = tid & 63;
-  __shared__ int sh_old;
-  // The hand-offs between workgroups (possibly on other XCDs) use agent-
-  // coherent (sc1) stores and loads for the data and an agent-scope atomic
-  // for the count: a writer's sc1 stores are complete (vmcnt(0)) before its
-  // workgroup counts in.  (Agent-scope fences instead write back and
-  // invalidate the whole L2 per wave: 74 vs 14 us for the head.)
-  auto arrive = [&](int* c) {   // the arrival index of this workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) sh_old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    return sh_old;
-  };
-  // 16-B agent-coherent load at int offset off of a wave-uniform base
-  auto ld_coh = [](wt_rsrc_t r, long off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off * 4), 0, 16);
-  };
-  const wt_rsrc_t part_r = wt_rsrc(part), f2p_r = wt_rsrc(f2p);
-  if (arrive(cnt + mb * NB + nb) != FC_S - 1) return;
-  if (tid == 0) __hip_atomic_store(cnt + mb * NB + nb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-
-  // ---- tile finisher: rows of the row block x this tile's 64 features
-  constexpr int R2 = 2 * RW, TPR = 256 / R2, FPT = 64 / TPR;
-  const int rl = tid / TPR, sub = tid % TPR;
-  const int row = mb * R2 + rl, fb = nb * 64 + sub * FPT;
-  int sacc[FC_N2];
-  float facc[FC_N2];
-#pragma unroll
-  for (int o = 0; o < FC_N2; ++o) { sacc[o] = 0; facc[o] = 0.f; }
-#pragma unroll
-  for (int c = 0; c < FPT / 8; ++c) {
-    const int f0 = fb + 8 * c;
-    v4i pv[FC_S][2];
-#pragma unroll
-    for (int s = 0; s < FC_S; ++s) {
-      const long off = ((long)s * m + row) * n + f0;
-      pv[s][0] = ld_coh(part_r, off);
-      pv[s][1] = ld_coh(part_r, off + 4);
-    }
-    const int4 c0 = *reinterpret_cast<const int4*>(hd.corr1 + f0), c1 = *reinterpret_cast<const int4*>(hd.corr1 + f0 + 4);
-    const float4 u0 = *reinterpret_cast<const float4*>(hd.u1 + f0), u4 = *reinterpret_cast<const float4*>(hd.u1 + f0 + 4);
-    const float4 v0 = *reinterpret_cast<const float4*>(hd.v1 + f0), v4 = *reinterpret_cast<const float4*>(hd.v1 + f0 + 4);
-    const float4 m0 = *reinterpret_cast<const float4*>(hd.m1 + f0), m4 = *reinterpret_cast<const float4*>(hd.m1 + f0 + 4);
-    int a[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-    for (int s = 0; s < FC_S; ++s)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[e] += pv[s][0][e];
-        a[4 + e] += pv[s][1][e];
-      }
-    const float uu[8] = {u0.x, u0.y, u0.z, u0.w, u4.x, u4.y, u4.z, u4.w};
-    const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v4.x, v4.y, v4.z, v4.w};
-    const float mm[8] = {m0.x, m0.y, m0.z, m0.w, m4.x, m4.y, m4.z, m4.w};
-    int q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = requant_one(a[e], uu[e], vv[e], mm[e], hd.z1, hd.lo1);
-    const uint32_t lo = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-    const uint32_t hw = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
-    if (!QDQ || y1) *reinterpret_cast<uint2*>(y1 + (long)row * n + f0) = make_uint2(lo, hw);
-    if constexpr (!QDQ) {
-      // exact sum_f (q1 - z1) w2[o][f] as in fc_finish_kernel (dot4 on the
-      // xor'd bytes plus (128 - z1) sum(w))
-      const int ql = (int)(lo ^ 0x80808080u), qh = (int)(hw ^ 0x80808080u);
-      const int zc = 128 - hd.z1;
-#pragma unroll
-      for (int o = 0; o < FC_N2; ++o) {
-        const uint2 wv = *reinterpret_cast<const uint2*>(hd.w2 + (long)(o < hd.n2 ? o : 0) * n + f0);
-        const int wx = (int)wv.x, wy = (int)wv.y;
-        const int wsum = __builtin_amdgcn_sdot4(wx, 0x01010101, __builtin_amdgcn_sdot4(wy, 0x01010101, 0, false), false);
-        sacc[o] += __builtin_amdgcn_sdot4(ql, wx, __builtin_amdgcn_sdot4(qh, wy, zc * wsum, false), false);
-      }
-    } else {
-      float xf[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = (float)(q[e] - hd.z1) * hd.s1;   // aten::dequantize
-        xf[e] = d > 0.f ? d : 0.f;                       // F.relu
-      }
-#pragma unroll
-      for (int o = 0; o < FC_N2; ++o) {
-        if (o < hd.n2) {
-          const float4 wa = *reinterpret_cast<const float4*>(hd.w2 + (long)o * n + f0);
-          const float4 wb = *reinterpret_cast<const float4*>(hd.w2 + (long)o * n + f0 + 4);
-          float t = facc[o];
-          t = __builtin_fmaf(xf[0], wa.x, t);
-          t = __builtin_fmaf(xf[1], wa.y, t);
-          t = __builtin_fmaf(xf[2], wa.z, t);
-          t = __builtin_fmaf(xf[3], wa.w, t);
-          t = __builtin_fmaf(xf[4], wb.x, t);
-          t = __builtin_fmaf(xf[5], wb.y, t);
-          t = __builtin_fmaf(xf[6], wb.z, t);
-          t = __builtin_fmaf(xf[7], wb.w, t);
-          facc[o] = t;
-        }
-      }
-    }
-  }
-  // the TPR lanes of a row (adjacent) sum their features by DPP
-#pragma unroll
-  for (int o = 0; o < FC_N2; ++o) {
-    if constexpr (!QDQ) {
-      sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0xB1, 0xF, 0xF, false);
-      if constexpr (TPR == 4) sacc[o] += __builtin_amdgcn_update_dpp(0, sacc[o], 0x4E, 0xF, 0xF, false);
-    } else {
-      facc[o] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, facc[o]), 0xB1, 0xF, 0xF, false));
-      if constexpr (TPR == 4)
-        facc[o] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, facc[o]), 0x4E, 0xF, 0xF, false));
-    }
-  }
-  static_assert(TPR == 2 || TPR == 4, "a row's lanes sit in one DPP quad");
-  if (sub == 0) {
-    const wt_rsrc_t fr = f2p_r;
-    const uint32_t b0 = (uint32_t)(((long)nb * m + row) * FC_N2 * 4);
-#pragma unroll
-    for (int g = 0; g < FC_N2 / 4; ++g) {
-      if constexpr (!QDQ)
-        store_wt16(fr, b0 + 16 * g, make_uint4(sacc[4 * g], sacc[4 * g + 1], sacc[4 * g + 2], sacc[4 * g + 3]));
-      else
-        store_wt16(fr, b0 + 16 * g,
-                   make_uint4(__builtin_bit_cast(uint32_t, facc[4 * g]), __builtin_bit_cast(uint32_t, facc[4 * g + 1]),
-                              __builtin_bit_cast(uint32_t, facc[4 * g + 2]),
-                              __builtin_bit_cast(uint32_t, facc[4 * g + 3])));
-    }
-  }
-  (void)lane;
-
-  // ---- row-block finisher: the last of the NB tile finishers of row block mb
-  if (arrive(cnt2 + mb) != NB - 1) return;
-  if (tid == 0) __hip_atomic_store(cnt2 + mb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // thread -> (row, OPT consecutive outputs); every feature block's partial
-  // sums in flight at once (16-B coherent loads), then summed in block order
-  constexpr int OPT = R2 * FC_N2 / 256, TPR2 = FC_N2 / OPT;
-  static_assert(OPT % 4 == 0, "16-B partial-sum loads");
-  const int r2 = mb * R2 + tid / TPR2, o0 = (tid % TPR2) * OPT;
-  v4i ps[FC_N1 / 64][OPT / 4];
-#pragma unroll
-  for (int b = 0; b < FC_N1 / 64; ++b)
-#pragma unroll
-    for (int j = 0; j < OPT / 4; ++j)
-      if (b < NB) ps[b][j] = ld_coh(f2p_r, ((long)b * m + r2) * FC_N2 + o0 + 4 * j);
-#pragma unroll
-  for (int e = 0; e < OPT; ++e) {
-    const int o = o0 + e;
-    if (o >= hd.n2) continue;
-    if constexpr (!QDQ) {
-      int tot = 0;
-#pragma unroll
-      for (int b = 0; b < FC_N1 / 64; ++b)
-        if (b < NB) tot += ps[b][e / 4][e % 4];
-      const int q2 = requant_one(tot, hd.u2[o], hd.v2[o], hd.m2[o], hd.z2, hd.lo2);
-      y2[(long)r2 * hd.n2 + o] = (uint8_t)q2;
-      y2f[(long)r2 * hd.n2 + o] = (float)(q2 - hd.z2) * hd.y2_scale;
-    } else {
-      float tot = 0.f;
-#pragma unroll
-      for (int b = 0; b < FC_N1 / 64; ++b)
-        if (b < NB) {
-          // (through an int: a bit_cast straight from the vector element read
-          // element 0 of every vector)
-          const int bits = ps[b][e / 4][e % 4];
-          tot += __builtin_bit_cast(float, bits);
-        }
-      y2f[(long)r2 * hd.n2 + o] = tot + (hd.b2 ? hd.b2[o] : 0.f);
-    }
-  }
-}
-
-// QCN_FC_FUSED=1 (A/B switch, off by default): the one-launch head.  It is
-// correct but slower — 26 vs 9 + 5 us at batch 1024, 14 vs 6 + 4 us at 256
-// (profiles/r03_diag_fc_fused_ab.txt): its finishing runs on the 64 last
-// arrivers after the split-K phase, against 1024 one-row waves in the
-// finisher launch, and every hand-off goes through memory-side (sc1) traffic.
-inline bool fc_fused() {
-  static const bool on = [] {
-    const char* e = std::getenv("QCN_FC_FUSED");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
-template <bool QDQ, class Head>
-void launch_fc_head(const uint8_t* x, int m, int k, const int8_t* w1, int n1, int* ws, const Head& hd,
-                    uint8_t* y1, uint8_t* y2, float* y2f, hipStream_t st) {
-  if (m < 1024) {
-    const int tiles = (m / 64) * (n1 / 64) * FC_S;
-    hipLaunchKernelGGL((fc_head_kernel<32, QDQ, Head>), dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, ws, hd,
-                       y1, y2, y2f);
-  } else {
-    const int tiles = (m / 128) * (n1 / 64) * FC_S;
-    hipLaunchKernelGGL((fc_head_kernel<64, QDQ, Head>), dim3(tiles), dim3(256), 0, st, x, m, k, w1, n1, ws, hd,
-                       y1, y2, y2f);
-  }
-}
-
 }  // namespace qcn
 
 extern "C" {
@@ -593,9 +347,7 @@ int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out) {
 
 long long qcn_classifier_workspace_size(int m, int n1) {
   if (m <= 0 || n1 <= 0) return 0;
-  // arrival counters, split-K partials, fc2 partial sums per 64-feature block
-  const long long nb = (n1 + 63) / 64;
-  return (long long)qcn::FC_CNT * 4 + (long long)qcn::FC_S * m * n1 * 4 + nb * m * qcn::FC_N2 * 4;
+  return (long long)qcn::FC_S * m * n1 * 4;   // the split-K partials
 }
 
 int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1, const float* u1,
@@ -608,18 +360,13 @@ int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1
     return QCN_ERR_ARG;
   if (m <= 0 || k <= 0 || n1 <= 0 || n2 <= 0 || y1_zp < 0 || y1_zp > 255 || y2_zp < 0 || y2_zp > 255)
     return QCN_ERR_ARG;
-  if (m % 128 != 0 || m > qcn::FC_MAXM || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 ||
+  if (m % 128 != 0 || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 ||
       n2 > qcn::FC_N2)
     return QCN_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  int* ws = static_cast<int*>(workspace);
-  int* part = ws + qcn::FC_CNT;
+  int* part = static_cast<int*>(workspace);
   qcn::FcHead hd{u1, v1, mult1, corr1, y1_zp, relu1 ? y1_zp : 0, w2, n2, u2, v2, mult2,
                  y2_zp, relu2 ? y2_zp : 0, y2_scale};
-  if (qcn::fc_fused()) {
-    qcn::launch_fc_head<false>(x, m, k, w1, n1, ws, hd, y1, y2, y2f, st);
-    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-  }
   qcn::launch_fc_splitk(x, m, k, w1, n1, part, st);
   hipLaunchKernelGGL(qcn::fc_finish_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd, y1,
                      y2, y2f);
@@ -634,17 +381,12 @@ int qcn_classifier_qdq_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, in
   if (!x || !w1 || !u1 || !v1 || !mult1 || !corr1 || !w2 || !workspace || !y2) return QCN_ERR_ARG;
   if (m <= 0 || k <= 0 || n1 <= 0 || n2 <= 0 || y1_zp < 0 || y1_zp > 255 || !(y1_scale > 0.f))
     return QCN_ERR_ARG;
-  if (m % 128 != 0 || m > qcn::FC_MAXM || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 ||
+  if (m % 128 != 0 || n1 != qcn::FC_N1 || k % (32 * qcn::FC_S * 8) != 0 ||
       n2 > qcn::FC_N2)
     return QCN_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  int* ws = static_cast<int*>(workspace);
-  int* part = ws + qcn::FC_CNT;
+  int* part = static_cast<int*>(workspace);
   qcn::FcHeadQdq hd{u1, v1, mult1, corr1, y1_zp, 0, y1_scale, w2, b2, n2};
-  if (qcn::fc_fused()) {
-    qcn::launch_fc_head<true>(x, m, k, w1, n1, ws, hd, y1, nullptr, y2, st);
-    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-  }
   qcn::launch_fc_splitk(x, m, k, w1, n1, part, st);
   hipLaunchKernelGGL(qcn::fc_finish_qdq_kernel, dim3((m + 3) / 4), dim3(256), 0, st, part, m, hd,
                      y1, y2);

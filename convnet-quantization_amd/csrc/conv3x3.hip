@@ -25,7 +25,6 @@
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
 #include <type_traits>
-#include <cstdlib>
 
 namespace qcn {
 
@@ -264,8 +263,7 @@ QCN_DEV v16i acc_init_corr(const int* __restrict__ corr, int co_base, int hi) {
 
 // Copy the staged [opx][cout] u8 tile (row stride OS) to its contiguous NHWC
 // destination with 16-B coalesced stores (full cache lines, no partial writes).
-// WT: write-through (the next launch reads it); plain stores keep the lines
-// in this XCD's L2 for a read-back by the same workgroup (conv3456).
+// WT: write-through (the next launch reads it); plain stores otherwise.
 template <int COUT, int OS, int NT, bool WT = true>
 QCN_DEV void store_staged(const uint8_t* lds_out, int opx, uint8_t* dst, long valid_px, int tid,
                           int rstride = COUT) {
@@ -490,37 +488,6 @@ struct WgBar {
   QCN_DEV void operator()() const { __syncthreads(); }
 };
 
-// Barrier of ONE half of an 8-wave workgroup (convpair_dual_kernel): the four
-// waves of a half synchronise among themselves through a counter in LDS, so
-// the two halves run independently (s_barrier would hold all eight waves).
-// Release: this wave's LDS writes are complete (lgkmcnt(0); the conv bodies
-// share no global memory between waves, and their barriers never drain VMEM —
-// in-flight weight prefetches stay in flight, as with __syncthreads).  Each
-// arrival adds 1; the k-th barrier completes at 4k.  The spin is bounded, so
-// a wave can never hang the launch (a miscount would give wrong results,
-// caught by the parity tests, not a stuck GPU).
-struct HalfBar {
-  uint32_t* ctr;      // this half's LDS counter
-  uint32_t target;    // 4 x barriers passed so far
-  int lane;
-  QCN_DEV void operator()() {
-    target += 4;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    wait_for(ctr, target);
-  }
-  QCN_DEV static void wait_for(uint32_t* c, uint32_t t) {
-    for (int spin = 0; spin < (1 << 22); ++spin) {
-      const uint32_t v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (__builtin_amdgcn_readfirstlane(v) >= t) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-};
-
 // ch0 / cstride: the workgroup's couts are channels ch0 .. ch0 + COUT - 1 of
 // an output with cstride channels per pixel (the cout-split conv6).
 template <class C, bool WT = true, class Bar = WgBar>
@@ -582,7 +549,7 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][C::JT], const ConvEpi& ep, uint8_t
 // unconditional batches (halo / tail lanes read a valid dummy address and are
 // replaced afterwards) so a thread keeps BATCH 16-B loads in flight instead of
 // one dependent HBM round trip per element.
-template <class C, bool BYPASS_L1 = false>
+template <class C>
 QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int n0, int y0,
                          uint8_t* patch, int tid) {
   constexpr int CIN = C::kCin;
@@ -608,12 +575,7 @@ QCN_DEV void stage_patch(const uint8_t* __restrict__ x, int nimg, int x_zp, int 
       inside[k] = n < nimg && yy >= 0 && yy < C::H && xx >= 0 && xx < C::W;
       dst[k] = (it < TOTAL && b0 + k < NITER) ? C::slot(seg, pr, pc) + chunk * 16 : -1;
       const long src = inside[k] ? (((long)n * C::H + yy) * C::W + xx) * CIN + chunk * 16 : 0;
-      if constexpr (BYPASS_L1) {   // nt: served by L2, never a stale L1 line
-        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(x + src));
-        v[k] = make_uint4((uint32_t)t[0], (uint32_t)t[1], (uint32_t)t[2], (uint32_t)t[3]);
-      } else {
-        v[k] = *reinterpret_cast<const uint4*>(x + src);
-      }
+      v[k] = *reinterpret_cast<const uint4*>(x + src);
     }
 #pragma unroll
     for (int k = 0; k < BATCH; ++k) {
@@ -765,15 +727,15 @@ QCN_DEV void pair_handoff(v16i (&acc)[CA::WI][CA::JT], const ConvEpi& epa, const
   }
 }
 
-template <class CA, class CB, bool BYPASS_L1 = false, bool WT = true>
+template <class CA, class CB>
 QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, int x_zp,
                            const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                            const int8_t* __restrict__ wb, ConvEpi epb,
                            uint8_t* __restrict__ y) {
   using P = PairCfg<CA, CB>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  // laundered: a caller that runs this body more than once (conv3456) must
-  // not get thread-id-derived addresses hoisted and held live across calls
+  // laundered: no thread-id-derived address is hoisted and held live across
+  // the two main loops
   int tid_l = threadIdx.x;
   asm volatile("" : "+v"(tid_l));
   const int tid = tid_l, lane = tid & 63, wave = tid >> 6;
@@ -784,7 +746,7 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
   stage_epik<CA::kCout, CA::NT>(epa, eka, tid);
   stage_epik<CB::kCout, CB::NT>(epb, ekb, tid);
-  stage_patch<CA, BYPASS_L1>(x, nimg, x_zp, n0, y0, lds, tid);
+  stage_patch<CA>(x, nimg, x_zp, n0, y0, lds, tid);
 
   v16i acc[CA::WI][CA::JT];
   conv_mainloop<CA>(lds, lds + CA::PATCH, wa, epa.corr, wave, lane, acc);
@@ -795,11 +757,11 @@ QCN_DEV void convpair_body(int tile, const uint8_t* __restrict__ x, int nimg, in
   __syncthreads();
   if constexpr (CA::WI == CB::WI && CA::JT == CB::JT) {
     conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, acc);
-    conv_epilogue<CB, WT>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+    conv_epilogue<CB>(acc, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
   } else {
     v16i accb[CB::WI][CB::JT];
     conv_mainloop<CB>(lds, lds + CB::PATCH, wb, epb.corr, wave, lane, accb);
-    conv_epilogue<CB, WT>(accb, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
+    conv_epilogue<CB>(accb, epb, lds, nimg, wave, lane, tid, y, tile, ekb);
   }
 }
 
@@ -966,8 +928,8 @@ QCN_DEV void convpair_ga_body(int tile, const uint8_t* __restrict__ x, int nimg,
                               const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   using P = PairGaCfg<CA, CB>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  // laundered: a caller that runs this body more than once (conv3456) must
-  // not get thread-id-derived addresses hoisted and held live across calls
+  // laundered: no thread-id-derived address is hoisted and held live across
+  // the two main loops
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
@@ -984,105 +946,6 @@ void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                         const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                         const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   convpair_ga_body<CA, CB, D>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
-}
-
-// --------------------------------------------------------------------------
-// Persistent pair with the next image's patch prefetched (conv3+conv4): each
-// workgroup takes tiles blockIdx.x, + gridDim.x, ...  The interior bytes of
-// the next tile's input patch (one whole image: CA::R x CA::W pixels) are
-// loaded into registers right after conv B's first weight loads — plain
-// loads the compiler counts, so B's loop waits only for its own — and land
-// in LDS (q ^ 0x80, plus the zero-point halo) after this tile's output is
-// stored: only the first tile pays the staging latency.
-template <class C>
-struct PatchPf {
-  static constexpr int PIECES = C::R * C::W * (C::kCin / 16);   // 16-B interior pieces
-  static constexpr int PER = (PIECES + C::NT - 1) / C::NT;
-  static_assert(C::SEGS == 1 && C::R == C::H && !C::kBand, "one whole image per tile");
-  uint4 v[PER];
-};
-
-template <class C>
-QCN_DEV void patch_pf_load(PatchPf<C>& pf, const uint8_t* __restrict__ x, int nimg, int n, int tid) {
-  constexpr int CH16 = C::kCin / 16;
-  const int nc = n < nimg ? n : nimg - 1;   // (past the end: a valid dummy image)
-  const uint8_t* img = x + (long)nc * C::IMG * C::kCin;
-#pragma unroll
-  for (int k = 0; k < PatchPf<C>::PER; ++k) {
-    int e = tid + k * C::NT;
-    e = e < PatchPf<C>::PIECES ? e : 0;
-    pf.v[k] = *reinterpret_cast<const uint4*>(img + (long)(e / CH16) * C::kCin + (e % CH16) * 16);
-  }
-}
-
-template <class C>
-QCN_DEV void patch_pf_store(const PatchPf<C>& pf, int x_zp, uint8_t* patch, int tid) {
-  constexpr int CH16 = C::kCin / 16;
-#pragma unroll
-  for (int k = 0; k < PatchPf<C>::PER; ++k) {
-    const int e = tid + k * C::NT;
-    if (e < PatchPf<C>::PIECES) {
-      const int px = e / CH16, chunk = e % CH16;
-      const uint4 v = pf.v[k];
-      *reinterpret_cast<uint4*>(patch + C::slot(0, px / C::W + 1, px % C::W + 1) + chunk * 16) =
-          make_uint4(xor80(v.x), xor80(v.y), xor80(v.z), xor80(v.w));
-    }
-  }
-  // zero-point halo: rows 0 and R+1, columns 0 and W+1
-  const uint32_t padw = xor80(splat_u8(x_zp));
-  constexpr int HALO = 2 * C::PCOLS + 2 * C::R;
-  for (int e = tid; e < HALO * CH16; e += C::NT) {
-    const int hs = e / CH16, chunk = e % CH16;
-    int pr, pc;
-    if (hs < C::PCOLS) { pr = 0; pc = hs; }
-    else if (hs < 2 * C::PCOLS) { pr = C::PROWS - 1; pc = hs - C::PCOLS; }
-    else { const int r = hs - 2 * C::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? C::PCOLS - 1 : 0; }
-    *reinterpret_cast<uint4*>(patch + C::slot(0, pr, pc) + chunk * 16) = make_uint4(padw, padw, padw, padw);
-  }
-}
-
-template <class CA, class CB, int D>
-__global__ __launch_bounds__(CA::NT, 2)
-void convpair_pipe_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                          const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
-                          const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
-  using P = PairGaCfg<CA, CB>;
-  static_assert(CA::PXB == CA::IMG, "one image per tile");
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
-  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
-  const int tid0 = threadIdx.x;
-  stage_epik<CA::kCout, CA::NT>(epa, eka, tid0);
-  stage_epik<CB::kCout, CB::NT>(epb, ekb, tid0);
-  const int G = (int)gridDim.x;
-  int t = (int)blockIdx.x;
-  if (t >= nimg) return;
-  stage_patch<CA>(x, nimg, x_zp, t, 0, lds, tid0);
-  for (; t < nimg; t += G) {
-    // laundered per tile (nothing thread-id-derived hoisted across the loop)
-    int tid = tid0;
-    asm volatile("" : "+v"(tid));
-    const int lane = tid & 63, wave = tid >> 6;
-    GaFrag<CA, D> ga;
-    ga_prefetch<CA, D>(ga, wa, wave, lane);
-    __syncthreads();   // this tile's patch complete
-    v16i acc[CA::WI][CA::JT];
-    conv_mainloop_ga<CA, D>(lds, wa, epa.corr, wave, lane, acc, ga);
-    GaFrag<CB, D> gb;
-    ga_prefetch<CB, D>(gb, wb, wave, lane);
-    const bool more = t + G < nimg;
-    PatchPf<CA> pf;
-    if (more) patch_pf_load<CA>(pf, x, nimg, t + G, tid);
-    pair_handoff<CA, CB>(acc, epa, eka, xb_zp, lds, wave, lane, tid);
-    __syncthreads();
-    v16i accb[CB::WI][CB::JT];
-    conv_mainloop_ga<CB, D>(lds, wb, epb.corr, wave, lane, accb, gb);
-    conv_epilogue<CB, true>(accb, epb, lds, nimg, wave, lane, tid, y, t, ekb);
-    if (more) {
-      __syncthreads();   // the staged output is read out before the next patch overwrites it
-      patch_pf_store<CA>(pf, x_zp, lds, tid);
-    }
-  }
 }
 
 // --------------------------------------------------------------------------
@@ -1133,103 +996,6 @@ void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                               const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                               const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
   convpair_ga_split_body<CA, CB, D, COUTB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
-}
-
-// --------------------------------------------------------------------------
-// Two independent halves in one 8-wave workgroup (one workgroup per CU,
-// persistent over tiles).  Waves 0-3 and waves 4-7 each run the
-// weights-from-L2 pair body on their own tiles and their own LDS patch region,
-// synchronising only among themselves (HalfBar), so a CU holds the same two
-// independent 4-wave streams as two co-resident workgroups — but their phase
-// offset is chosen: half 1 starts once half 0 has passed `offset_bar` of its
-// barriers, so one half's staging and epilogues run beside the other half's
-// MFMA loops instead of wherever two workgroups happen to drift.
-template <class CA, class CB>
-struct DualCfg {
-  static constexpr int PATCH = PairGaCfg<CA, CB>::PATCH;   // per half
-  static constexpr int OFF_EA = 0;
-  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
-  static constexpr int OFF_CTR = OFF_EB + 12 * CB::kCout;
-  static constexpr int OFF_H = OFF_CTR + 16;
-  static constexpr int LDS = OFF_H + 2 * PATCH;
-  static_assert(OFF_H % 16 == 0 && PATCH % 16 == 0, "16-B aligned regions");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
-template <class CA, class CB, int D>
-__global__ __launch_bounds__(2 * CA::NT, 1)
-void convpair_dual_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                          const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
-                          const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y,
-                          int offset_bar) {
-  using P = DualCfg<CA, CB>;
-  static_assert(CA::NT == 256, "4-wave halves");
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
-  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(lds + P::OFF_CTR);
-  stage_epik<CA::kCout, 2 * CA::NT>(epa, eka, (int)threadIdx.x);
-  stage_epik<CB::kCout, 2 * CA::NT>(epb, ekb, (int)threadIdx.x);
-  if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
-  __syncthreads();
-  int tid = (int)threadIdx.x & 255;
-  asm volatile("" : "+v"(tid));
-  const int half = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
-  uint8_t* lb = lds + P::OFF_H + half * P::PATCH;
-  HalfBar bar{ctr + half, 0u, tid & 63};
-  const int b = (int)blockIdx.x, G = (int)gridDim.x;
-  const long ntile = ((long)nimg * CA::IMG + CA::PXB - 1) / CA::PXB;
-  // half 1 starts behind half 0 (only if half 0 has a tile to pass barriers in)
-  if (half == 1 && offset_bar > 0 && b < ntile) HalfBar::wait_for(ctr, 4u * (uint32_t)offset_bar);
-  for (long t = b + (long)half * G; t < ntile; t += 2L * G) {
-    // laundered per tile: nothing thread-id-derived is hoisted out of the loop
-    // and held live across the tile (the body needs every register)
-    int ltid = tid;
-    asm volatile("" : "+v"(ltid));
-    convpair_ga_tile<CA, CB, D>((int)t, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, lb, eka, ekb, ltid, bar);
-    bar();   // the staged output is read out before the next tile's patch overwrites it
-  }
-}
-
-// --------------------------------------------------------------------------
-// conv3 -> conv4 -> conv5 -> conv6 in one launch.  Each 4-wave workgroup owns
-// two images: conv3+4 of the first (LDS weight ring, as convpair_kernel),
-// conv3+4 of the second, then conv5+6 of both (weights from L2,
-// convpair_ga_body).  a4 goes out to HBM/L2 with plain stores and comes back
-// into conv5's patch in the same workgroup (16 KB per workgroup, no other
-// workgroup reads it: no inter-workgroup hand-off).  Two workgroups per CU
-// run independently, and the grid is one round of workgroups, so the launch
-// pays one dispatch ramp and drain instead of two kernels' worth.
-template <class C3, class C4, class C5, class C6, int D>
-struct Conv3456Cfg {
-  static_assert(C3::NT == C5::NT && C4::kCout == C5::kCin && C4::kPool && C4::W / 2 == C5::W,
-                "conv4's pooled output is conv5's input");
-  static_assert(C5::SEGS == 2 && C3::SEGS == 1, "two images per workgroup, one per conv3+4 pass");
-  static constexpr int L34 = PairCfg<C3, C4>::LDS, L56 = PairGaCfg<C5, C6>::LDS;
-  static constexpr int LDS = L34 > L56 ? L34 : L56;
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
-};
-
-template <class C3, class C4, class C5, class C6, int D>
-__global__ __launch_bounds__(C3::NT, 2)
-void conv3456_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
-                     const int8_t* __restrict__ w3, ConvEpi ep3, int z4in,
-                     const int8_t* __restrict__ w4, ConvEpi ep4, uint8_t* __restrict__ a4, int z5in,
-                     const int8_t* __restrict__ w5, ConvEpi ep5, int z6in,
-                     const int8_t* __restrict__ w6, ConvEpi ep6, uint8_t* __restrict__ y) {
-  const int t = (int)blockIdx.x;
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    const int n = 2 * t + k;
-    if (n < nimg) {
-      convpair_body<C3, C4, false, false>(n, x, nimg, x_zp, w3, ep3, z4in, w4, ep4, a4);
-    }
-    // this image's a4 stores retired (the read-back below and the next
-    // image's LDS staging follow)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  convpair_ga_body<C5, C6, D>(t, a4, nimg, z5in, w5, ep5, z6in, w6, ep6, y);
 }
 
 // --------------------------------------------------------------------------
@@ -1897,21 +1663,6 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-template <class CA, class CB, int D>
-int launch_pair_pipe(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
-                     int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st,
-                     int wg_per_cu) {
-  using P = PairGaCfg<CA, CB>;
-  const int ncu = qcn_cu_count();
-  if (ncu <= 0) return QCN_ERR_HIP;
-  const int grid = nimg < wg_per_cu * ncu ? nimg : wg_per_cu * ncu;
-  auto k = convpair_pipe_kernel<CA, CB, D>;
-  static bool attr_done[QCN_MAX_DEV] = {};
-  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
-  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-}
-
 template <class CA, class CB, int D, int COUTB>
 int launch_pair_ga_split(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
                          int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
@@ -1923,29 +1674,6 @@ int launch_pair_ga_split(const uint8_t* x, int nimg, int x_zp, const int8_t* wa,
   if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
   hipLaunchKernelGGL(k, dim3(grid), dim3(CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-}
-
-template <class CA, class CB, int D>
-int launch_pair_dual(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
-                     int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st,
-                     int offset_bar) {
-  using P = DualCfg<CA, CB>;
-  const long ntile = ((long)nimg * CA::IMG + CA::PXB - 1) / CA::PXB;
-  const int ncu = qcn_cu_count();
-  if (ncu <= 0) return QCN_ERR_HIP;
-  // one workgroup per CU, two tiles in flight per workgroup
-  const int grid = (int)(ntile < 2L * ncu ? (ntile + 1) / 2 : ncu);
-  auto k = convpair_dual_kernel<CA, CB, D>;
-  static bool attr_done[QCN_MAX_DEV] = {};
-  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(2 * CA::NT), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb,
-                     y, offset_bar);
-  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
 }
 
 // Tuned instantiations: the SimpleConvNet layers and the
@@ -2065,124 +1793,35 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   // CU for conv3+conv4).  ConvCfg's WI = 4 (128 x 128 tiles, one wave per
   // SIMD, a third fewer LDS bytes per MFMA) measured slower with no partner
   // wave to cover the epilogues (63 vs 53 us, 56 vs 51 us) and is not built.
+  const int ncu = qcn_cu_count();
+  if (ncu <= 0) return QCN_ERR_HIP;
   if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
-    // QCN_PAIR34 (A/B switch): 0 = LDS weight ring, D >= 1 = weights from L2
-    // into registers D K-steps ahead (both waves of a cout block load them)
-    static const int impl34 = [] {
-      const char* e = std::getenv("QCN_PAIR34");
-      return e ? std::atoi(e) : 0;
-    }();
-    using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
-    using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
-    static const int off34 = env_int("QCN_DUAL_OFFSET34", 2);
-    if (impl34 == 12) return launch_pair_dual<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
-    if (impl34 == 13) return launch_pair_dual<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off34);
     // one image per CU or fewer (config 2): eight waves per image — conv3 as
     // 64-cout x 64-pixel wave tiles, conv4 as 32-cout x 128-pixel tiles — so
     // each SIMD holds two waves of the image's work instead of one
-    // (QCN_SMALL34: images per CU at or below which; 0 = never)
-    static const int small34 = env_int("QCN_SMALL34", 1);
-    const int ncu34 = qcn_cu_count();
-    if (impl34 == 0 && ncu34 > 0 && nimg <= small34 * ncu34)
+    if (nimg <= ncu)
       return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl34 == 22) return launch_pair_pipe<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, 2);
-    if (impl34 == 23) return launch_pair_pipe<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, 2);
-    if (impl34 == 2) return launch_pair_ga<A3, B4, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl34 == 3) return launch_pair_ga<A3, B4, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl34 == 4) return launch_pair_ga<A3, B4, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
                        ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
-    // four images per 8-wave workgroup (one per CU: the conv6 patch and ring
-    // fill the LDS); below four images per CU that leaves CUs idle, so small
-    // batches take two images per 4-wave workgroup (same wave tile and
-    // patch layout, twice the workgroups)
-    // QCN_PAIR56 (A/B switch): 0 = LDS weight ring (8-wave, 4 images per
-    // workgroup), D >= 1 = weights from L2 into registers D K-steps ahead
-    // (4-wave, 2 images per workgroup, two workgroups per CU)
-    static const int impl56 = [] {
-      const char* e = std::getenv("QCN_PAIR56");
-      return e ? std::atoi(e) : 4;
-    }();
+    // two images per 4-wave workgroup, two workgroups per CU, weights from L2
+    // into registers 4 K-steps ahead (convpair_ga_kernel)
     using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
     using B1 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
-    if (impl56 == 1) return launch_pair_ga<A1, B1, 1>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl56 == 2) return launch_pair_ga<A1, B1, 2>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl56 == 3) return launch_pair_ga<A1, B1, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    static const int off56 = env_int("QCN_DUAL_OFFSET56", 2);
-    if (impl56 == 13) return launch_pair_dual<A1, B1, 3>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off56);
-    if (impl56 == 14) return launch_pair_dual<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, off56);
-    // below one two-image workgroup per CU, split conv6's couts over two
-    // workgroups (conv5 computed by both): twice the workgroups
-    // (QCN_SPLIT56: images per CU at or below which to split; 0 = never).
-    // Batch 256: 22.3 -> 20.6-21.7 us; batch 512 (one workgroup per CU
-    // either way) 27.9 -> 33.3 us, so only at <= 1 image per CU
-    static const int split56 = env_int("QCN_SPLIT56", 1);
-    const int ncu56 = qcn_cu_count();
-    if (impl56 >= 1 && impl56 <= 5 && ncu56 > 0 && nimg <= split56 * ncu56)
+    // at or below one image per CU, conv6's couts split over two workgroups
+    // (conv5 computed by both): twice the workgroups.  Batch 256: 22.3 ->
+    // 20.6-21.7 us; batch 512 (one workgroup per CU either way) 27.9 -> 33.3
+    // us, so only at <= 1 image per CU
+    if (nimg <= ncu)
       return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl56 == 4) return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    if (impl56 == 5) return launch_pair_ga<A1, B1, 5>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    const int ncu = qcn_cu_count();
-    if (ncu > 0 && nimg < 4 * ncu)
-      return launch_pair<ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>,
-                         ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>>(
-          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    return launch_pair<ConvCfg<128, 256, 8, false, 2, 16, 224, 0, false>,
-                       ConvCfg<256, 256, 8, true, 2, 16, 32, 64, true>>(
-        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;
-}
-
-// ConvEpi of one qcn_conv_layer_t; *zin receives the next layer's input zp.
-static int layer_epi(const qcn_conv_layer_t* l, int cout, ConvEpi& ep, int& zin) {
-  if (!l || !l->w_packed || !l->u || !l->v || !l->mult || !l->corr || l->cout != cout) return QCN_ERR_ARG;
-  if (l->y_zp < 0 || l->y_zp > 255) return QCN_ERR_ARG;
-  ep = ConvEpi{l->u, l->v, l->mult, l->corr, l->y_zp, l->relu ? l->y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
-  zin = l->y_zp;
-  if (l->qdq) {
-    ep.qdq = 1;
-    ep.s1 = l->qdq->s1; ep.z1 = l->qdq->z1; ep.inv2 = l->qdq->inv2; ep.z2 = l->qdq->z2;
-    zin = l->qdq->z2;
-  }
-  return QCN_OK;
-}
-
-int qcn_conv3456_u8s8(const uint8_t* x, int nimg, int x_zp, const qcn_conv_layer_t* l3,
-                      const qcn_conv_layer_t* l4, const qcn_conv_layer_t* l5,
-                      const qcn_conv_layer_t* l6, uint8_t* a4, int kmajor, uint8_t* y,
-                      void* stream) {
-  if (!x || !a4 || !y || nimg <= 0 || x_zp < 0 || x_zp > 255) return QCN_ERR_ARG;
-  if (!l3 || !l4 || !l5 || !l6) return QCN_ERR_ARG;
-  if (l3->cout != 128 || l4->cout != 128 || l5->cout != 256 || l6->cout != 256) return QCN_ERR_UNSUPPORTED;
-  ConvEpi e3, e4, e5, e6;
-  int z4, z5, z6, zo;
-  int rc;
-  if ((rc = layer_epi(l3, 128, e3, z4)) || (rc = layer_epi(l4, 128, e4, z5)) ||
-      (rc = layer_epi(l5, 256, e5, z6)) || (rc = layer_epi(l6, 256, e6, zo)))
-    return rc;
-  if (kmajor && (long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
-  e6.kmajor = kmajor ? 1 : 0;
-  using C3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
-  using C4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
-  using C5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
-  using C6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
-  constexpr int D = 4;
-  using K = Conv3456Cfg<C3, C4, C5, C6, D>;
-  auto k = conv3456_kernel<C3, C4, C5, C6, D>;
-  static bool attr_done[QCN_MAX_DEV] = {};
-  if (!qcn_set_lds_once((const void*)k, K::LDS, attr_done)) return QCN_ERR_HIP;
-  const int grid = (nimg + 1) / 2;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(C3::NT), K::LDS, (hipStream_t)stream, x, nimg, x_zp,
-                     l3->w_packed, e3, z4, l4->w_packed, e4, a4, z5, l5->w_packed, e5, z6,
-                     l6->w_packed, e6, y);
-  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
 int qcn_conv3x3_u8s8_kmajor(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,

@@ -21,7 +21,6 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace qcn {
@@ -1044,14 +1043,6 @@ inline int dispatch_stream_s2(GemmArgs& a, hipStream_t st) {
 
 template <bool RESID>
 int dispatch_stream(GemmArgs& a, hipStream_t st) {
-  static const bool bl128 = [] {
-    const char* e = std::getenv("QCN_STREAM_BL128");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  static const bool bl64 = [] {   // A/B switch: K = 64 through the ring too
-    const char* e = std::getenv("QCN_STREAM_BL64");
-    return e && std::atoi(e) != 0;
-  }();
   // 32-bit buffer offsets
   if (a.npix * (long)(a.cin > a.cout ? a.cin : a.cout) >= (1L << 31) - 4096) return -1;
   if (a.cout % 128 != 0) {
@@ -1064,8 +1055,10 @@ int dispatch_stream(GemmArgs& a, hipStream_t st) {
     }
   }
   switch (a.cin) {
-    case 64: return bl64 ? stream_modes<64, 4, RESID, 4, true>(a, st) : stream_modes<64, 4, RESID, 4, false>(a, st);
-    case 128: return bl128 ? stream_modes<128, 4, RESID, 4, true>(a, st) : stream_modes<128, 4, RESID, 3, false>(a, st);
+    // K = 64 keeps its activations in registers (through the LDS-DMA ring it
+    // measured slower); K >= 128 streams them through the ring
+    case 64: return stream_modes<64, 4, RESID, 4, false>(a, st);
+    case 128: return stream_modes<128, 4, RESID, 4, true>(a, st);
     case 256: return stream_modes<256, 4, RESID, 4, true>(a, st);
     case 512: return stream_modes<512, 4, RESID, 3, true>(a, st);
     default: return -1;
@@ -1107,38 +1100,24 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   if ((long)((a.npix + 255) / 256) * (cout / 64) >= (1L << 31)) return QCN_ERR_UNSUPPORTED;
   if (a.npix >= (1L << 31) - 256) return QCN_ERR_UNSUPPORTED;   // 32-bit pixel indices in the kernel
   hipStream_t st = (hipStream_t)stream;
-  // thin 1x1 stride-1 convs (K = Cin <= QCN_GEMM_STREAM, default 512; 0 =
-  // tiled kernel only) stream: ResNet-50 98.3-99.0 -> 102.9-104.1 K img/s
-  // (K <= 256) and 104.0-105.4 -> 105.9-108.3 K (K <= 512) on two boxes
-  // (profiles/r03_diag_resnet_stream_ab.txt)
-  static const int stream_k = [] {
-    const char* e = std::getenv("QCN_GEMM_STREAM");
-    return e ? std::atoi(e) : 512;
-  }();
+  // thin 1x1 stride-1 convs (K = Cin <= 512) stream: ResNet-50 98.3-99.0 ->
+  // 102.9-104.1 K img/s (K <= 256) and 104.0-105.4 -> 105.9-108.3 K (K <= 512)
+  // on two boxes (profiles/r03_diag_resnet_stream_ab.txt)
+  constexpr int stream_k = 512;
   if (cin <= stream_k && kh == 1 && kw == 1 && stride_h == 1 && stride_w == 1 && pad_h == 0 && pad_w == 0) {
     const int rc = resid ? qcn::dispatch_stream<true>(a, st) : qcn::dispatch_stream<false>(a, st);
     if (rc >= 0) return rc;
   }
-  // whole-image 3x3 for the 14x14x256 and 7x7x512 maps (QCN_GEMM_IMG3=0: tiled)
-  // (QCN_GEMM_IMG3: 0 = tiled, 1 = the 14x14x256 maps only, 2 = also the
-  // 7x7x512 maps).  Same box: layer-3 3x3 0.101 -> 0.065 ms, layer-4 0.094 ->
-  // 0.073 ms, ResNet-50 108.6-109.3 -> 114.5-114.6 K img/s
-  // (profiles/r03_diag_resnet_img3_ab.txt)
-  static const int img3 = [] {
-    const char* e = std::getenv("QCN_GEMM_IMG3");
-    return e ? std::atoi(e) : 2;
-  }();
-  if (img3 && !resid && kh == 3 && kw == 3 && stride_h == 1 && stride_w == 1 && pad_h == 1 && pad_w == 1 &&
+  // whole-image 3x3 for the 14x14x256 and 7x7x512 maps.  Same box: layer-3
+  // 3x3 0.101 -> 0.065 ms, layer-4 0.094 -> 0.073 ms, ResNet-50 108.6-109.3
+  // -> 114.5-114.6 K img/s (profiles/r03_diag_resnet_img3_ab.txt)
+  if (!resid && kh == 3 && kw == 3 && stride_h == 1 && stride_w == 1 && pad_h == 1 && pad_w == 1 &&
       h == w && cout % 256 == 0) {
     if (h == 14 && cin == 256) return qcn::launch_img<14, 256, 8, 1>(a, st);
-    if (h == 7 && cin == 512 && img3 == 2) return qcn::launch_img<7, 512, 8, 1>(a, st);
+    if (h == 7 && cin == 512) return qcn::launch_img<7, 512, 8, 1>(a, st);
   }
-  // the stride-2 downsample 1x1 streams too (QCN_GEMM_STREAM_S2=0: tiled)
-  static const bool stream_s2 = [] {
-    const char* e = std::getenv("QCN_GEMM_STREAM_S2");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  if (stream_s2 && cin <= stream_k && !resid && kh == 1 && kw == 1 && stride_h == 2 && stride_w == 2 &&
+  // the stride-2 downsample 1x1 streams too
+  if (cin <= stream_k && !resid && kh == 1 && kw == 1 && stride_h == 2 && stride_w == 2 &&
       pad_h == 0 && pad_w == 0) {
     const int rc = qcn::dispatch_stream_s2(a, st);
     if (rc >= 0) return rc;
@@ -1149,15 +1128,6 @@ extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w,
   // (profiles/r02_diag_resnet_bn256_layers.txt)
   if (cout % 256 == 0 && !resid && (kh * kw > 1 || cin >= 2048))
     return qcn::launch_gemm<256, false>(a, st);
-  // thin convs (K <= QCN_GEMM_THIN_K) on 128-pixel tiles, three workgroups per
-  // CU. Off by default: the layer-1 expand 1x1s (K = 64) went 0.236 -> 0.278 ms
-  // on them, ResNet-50 100.8 -> 96.0 K img/s (profiles/r03_diag_resnet_thin_ab.txt)
-  static const int thin_k = [] {
-    const char* e = std::getenv("QCN_GEMM_THIN_K");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (cout % 128 == 0 && a.kcs * 32 <= thin_k)
-    return resid ? qcn::launch_gemm<128, true, 128>(a, st) : qcn::launch_gemm<128, false, 128>(a, st);
   if (cout % 128 == 0)
     return resid ? qcn::launch_gemm<128, true>(a, st) : qcn::launch_gemm<128, false>(a, st);
   return resid ? qcn::launch_gemm<64, true>(a, st) : qcn::launch_gemm<64, false>(a, st);

@@ -30,7 +30,6 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
-#include <cstdlib>
 
 namespace qcn {
 
@@ -294,18 +293,6 @@ int launch_stem(const qcn::StemArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((qcn::stem_fused_kernel<S, P>), dim3(grid), dim3(C::NTH), C::LDS, st, a);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
-// Pool rows per band at 224² (QCN_STEM_P, an A/B switch): 4 by default — a
-// band of 9 conv rows recomputes one shared conv row per 8 instead of per 4
-// and passes its three barriers half as often per image: 0.422 -> 0.329 ms,
-// ResNet-50 106.2-108.2 -> 108.3-109.0 K img/s same box (1 pool row, two
-// workgroups per CU at 128 VGPRs, 0.549 ms; profiles/r03_diag_resnet_stem_band_ab.txt)
-int stem_band_rows() {
-  static const int p = [] {
-    const char* e = std::getenv("QCN_STEM_P");
-    return e && std::atoi(e) == 2 ? 2 : 4;
-  }();
-  return p;
-}
 }  // namespace
 
 extern "C" int qcn_resnet_stem_fused(const float* x, int nimg, int h, int w, float in_scale,
@@ -323,5 +310,10 @@ extern "C" int qcn_resnet_stem_fused(const float* x, int nimg, int h, int w, flo
   a.u = u; a.v = v; a.mult = mult; a.corr = corr; a.zp_y = y_zp; a.lo = relu ? y_zp : 0; a.y = y;
   hipStream_t st = (hipStream_t)stream;
   if (h == 64) return launch_stem<64>(a, st);
-  return stem_band_rows() == 2 ? launch_stem<224, 2>(a, st) : launch_stem<224, 4>(a, st);
+  // 4 pool rows per band at 224²: a band of 9 conv rows recomputes one shared
+  // conv row per 8 instead of per 4 (2 pool rows) and passes its three
+  // barriers half as often per image: 0.422 -> 0.329 ms, ResNet-50
+  // 106.2-108.2 -> 108.3-109.0 K img/s same box (1 pool row, two workgroups
+  // per CU at 128 VGPRs: 0.549 ms; profiles/r03_diag_resnet_stem_band_ab.txt)
+  return launch_stem<224, 4>(a, st);
 }

@@ -29,13 +29,6 @@ class QDQ(C.Structure):
     _fields_ = [("s1", C.c_float), ("z1", C.c_int32), ("inv2", C.c_float), ("z2", C.c_int32)]
 
 
-class ConvLayer(C.Structure):
-    """qcn_conv_layer_t"""
-    _fields_ = [("w_packed", C.c_void_p), ("cout", C.c_int), ("u", C.c_void_p), ("v", C.c_void_p),
-                ("mult", C.c_void_p), ("corr", C.c_void_p), ("y_zp", C.c_int), ("relu", C.c_int),
-                ("qdq", C.POINTER(QDQ))]
-
-
 vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_longlong
@@ -67,8 +60,6 @@ SIGNATURES = {
     "qcn_conv3x3_pair_u8s8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
                                     C.POINTER(QDQ), vp, i32, vp, vp, vp, vp, i32, i32,
                                     C.POINTER(QDQ), i32, vp, vp]),
-    "qcn_conv3456_u8s8": (i32, [vp, i32, i32, C.POINTER(ConvLayer), C.POINTER(ConvLayer),
-                                C.POINTER(ConvLayer), C.POINTER(ConvLayer), vp, i32, vp, vp]),
     "qcn_conv3x3_u8s8_kmajor": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
                                       i32, vp, vp]),
     "qcn_classifier_u8s8": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32, vp, i32, vp, vp,

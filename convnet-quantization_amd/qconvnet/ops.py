@@ -198,9 +198,8 @@ def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=F
 
 
 def classifier_workspace(m, n1, device):
-    # zero-filled once: the one-launch head's arrival counters live at its end
-    # (each launch leaves them at zero again)
-    return torch.zeros(lib().qcn_classifier_workspace_size(m, n1), dtype=torch.uint8, device=device)
+    """The head's int32 split-K partials (no initialisation needed)."""
+    return torch.empty(lib().qcn_classifier_workspace_size(m, n1), dtype=torch.uint8, device=device)
 
 
 def pack_fc_kmajor(w: np.ndarray):
@@ -239,30 +238,6 @@ def conv_pair(x, la, lb, out, kmajor=False):
     if rc == _lib.QCN_ERR_UNSUPPORTED:
         return False
     check(rc, "conv_pair")
-    return True
-
-
-def _layer(d):
-    return _lib.ConvLayer(d.w.data_ptr(), d.cout, d.u.data_ptr(), d.v.data_ptr(), d.mult.data_ptr(),
-                          d.corr.data_ptr(), int(d.z_y), int(bool(d.relu)),
-                          C.pointer(d.qdq) if d.qdq is not None else None)
-
-
-def conv3456(x, l3, l4, l5, l6, a4, out, kmajor=False):
-    """conv3+conv4 (pool) + conv5+conv6 (pool) in one launch (qcn_conv3456_u8s8).
-    ``a4`` receives conv4's pooled output (u8 NHWC [n,8,8,128]).  Returns False
-    when the channel counts are not SimpleConvNet's."""
-    _need(x, torch.uint8, "conv3456.x")
-    _need(a4, torch.uint8, "conv3456.a4")
-    n, h, w, cin = x.shape
-    if (h, w, cin) != (16, 16, 64) or tuple(a4.shape) != (n, 8, 8, 128):
-        return False
-    L = [_layer(d) for d in (l3, l4, l5, l6)]
-    rc = lib().qcn_conv3456_u8s8(_ptr(x), n, int(l3.z_x), *(C.byref(t) for t in L), _ptr(a4),
-                                 int(bool(kmajor)), _ptr(out), _stream())
-    if rc == _lib.QCN_ERR_UNSUPPORTED:
-        return False
-    check(rc, "conv3456")
     return True
 
 
@@ -393,8 +368,7 @@ def conv(x, x_zp, layer, out=None, resid=None, impl=None):
     kh, kw, stride (sy, sx), pad (py, px), u, v, mult, corr, z_y, s_y, relu.
     ``resid=(r, s_r, z_r, s_out, z_out)`` fuses the bottleneck's residual join
     (GEMM kernel only).  impl: "gemm" (LDS-tiled, default) or "gen" (the
-    register-direct kernel; QCN_CONV_IMPL overrides the default)."""
-    import os
+    register-direct kernel, a second implementation parity-tested beside it)."""
     _need(x, torch.uint8, "conv.x")
     n, h, w, cin = x.shape
     d = layer
@@ -402,7 +376,7 @@ def conv(x, x_zp, layer, out=None, resid=None, impl=None):
     ow = (w + 2 * d.px - d.kw) // d.sx + 1
     if out is None:
         out = torch.empty((n, oh, ow, d.cout), dtype=torch.uint8, device=x.device)
-    impl = impl or os.environ.get("QCN_CONV_IMPL", "gemm")
+    impl = impl or "gemm"
     if impl == "gen" and resid is None:
         check(lib().qcn_conv_u8s8_nhwc(_ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, d.kh,
                                        d.kw, d.sy, d.sx, d.py, d.px, _ptr(d.u), _ptr(d.v),

@@ -23,7 +23,6 @@ plus torch.ao prepare/convert with MinMax observers (observer.py:349-427).
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -217,7 +216,8 @@ class QuantizedConvNet:
         self.is_custom_quantized = self.mode == "qdq"
         self.host_io = False
         self.fuse12 = fuse12
-        self.fuse_pairs = True
+        self.fuse_pairs = True   # conv3+conv4 / conv5+conv6 as one launch each
+        self.fc_head = True      # fc1 -> fc2 as the split-K head (False: two linear launches)
         self._bufs = {}
         self._graphs = {}
         self._upload()
@@ -305,10 +305,7 @@ class QuantizedConvNet:
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
-            if self._block34(2 if self._fused(x_shape) else 1):
-                names[names.index("conv3"):names.index("conv6") + 1] = ["conv3456"]
-            else:
-                names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
+            names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
         if self._head(x_shape[0], keep):
             names = names[:-2] + ["fc12"]
         return tuple(names)
@@ -317,17 +314,11 @@ class QuantizedConvNet:
         """conv3+conv4 and conv5+conv6 as fused block launches (their middle
         activation stays in LDS); keep=True runs them per layer so every
         activation is inspectable."""
-        return self.fuse_pairs and not keep and os.environ.get("QCN_PAIRS", "1") == "1"
-
-    def _block34(self, first):
-        """conv3..conv6 as ONE launch (qcn_conv3456_u8s8) behind the fused
-        conv12 when QCN_CONV3456=1 (A/B switch; measured slower than the two
-        pair launches, 99.2 vs 95.5 us, so off by default)."""
-        return first == 2 and os.environ.get("QCN_CONV3456", "0") == "1"
+        return self.fuse_pairs and not keep
 
     def _head_fused(self, n):
         f1, f2 = self.fc1, self.fc2
-        if os.environ.get("QCN_FC_HEAD", "fused") == "linear":   # A/B switch (tools/ab.sh)
+        if not self.fc_head:
             return False
         c6 = self.L[5]
         common = (n % 128 == 0 and f1.w.shape[0] == 512 and f1.w.shape[1] == 4096 and
@@ -382,19 +373,6 @@ class QuantizedConvNet:
             mark()
             prev, first = b["a1"], 1
         pairs = self._pairs(keep)
-        if pairs and self._block34(first):
-            # conv3..conv6 in one launch (conv4's pooled output round-trips
-            # through b["a4"] inside the launch)
-            if head:
-                if "a6k" not in b:
-                    b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
-                out, km = b["a6k"], True
-            else:
-                out, km = b["a6"], False
-            if not ops.conv3456(prev, L[2], L[3], L[4], L[5], b["a4"], out, kmajor=km):
-                raise RuntimeError("fused conv3..conv6 rejected a supported shape")
-            mark()
-            prev, first = out, 6
         for i in range(first, 6):
             d = L[i]
             if pairs and i in (2, 4):   # conv3+conv4, conv5+conv6 in one launch each

@@ -19,7 +19,6 @@ kernel on the current stream, capturable into a HIP graph):
 """
 from __future__ import annotations
 
-import os
 import re
 
 import numpy as np
@@ -205,8 +204,7 @@ class QuantizedResNet:
 
     def _conv3x3_halo(self, y, d):
         n, h, w, cin = y.shape
-        if (d.w64 is None or h != w or (h, cin, d.cout) not in self.HALO_SHAPES
-                or os.environ.get("QCN_RESNET_HALO", "1") != "1"):
+        if d.w64 is None or h != w or (h, cin, d.cout) not in self.HALO_SHAPES:
             return None
         return ops.conv3x3(y, d.z_x, d.w64, d.cout, d.u, d.v, d.mult, d.corr, d.z_y, d.relu, False)
 
@@ -231,10 +229,9 @@ class QuantizedResNet:
 
     def _stem_fusable(self, x):
         """The one-launch stem (qcn_resnet_stem_fused) covers torchvision's
-        7x7/2 pad-3 64-channel stem at 224x224 and 64x64 inputs;
-        QCN_STEM_FUSED=0 selects the three-launch form."""
+        7x7/2 pad-3 64-channel stem at 224x224 and 64x64 inputs."""
         e = self.spec["stem"]
-        return (os.environ.get("QCN_STEM_FUSED", "1") == "1" and self.stem.cout == 64
+        return (self.stem.cout == 64
                 and tuple(np.asarray(e["w"]).shape[1:]) == (3, 7, 7)
                 and tuple(e["stride"]) == (2, 2) and tuple(e["pad"]) == (3, 3)
                 and x.shape[1] == 3 and x.shape[2] == x.shape[3] and x.shape[2] in (224, 64))
@@ -322,7 +319,6 @@ class QuantizedResNet:
             yield
         if keep:
             inter["stem"] = q
-        fuse = os.environ.get("QCN_RESID_FUSED", "1") == "1"
         for i, (b, e) in enumerate(zip(self.blocks, sp["blocks"])):
             zx = b["c1"].z_x
             if b["ds"] is not None:   # identity first, so conv3 can consume it
@@ -340,16 +336,10 @@ class QuantizedResNet:
             mark("conv")
             yield
             so, zo = e["out"]
-            if fuse:   # conv3 + residual join in one launch
-                q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
-                mark("conv")
-                yield
-            else:
-                y = ops.conv(y, b["c3"].z_x, b["c3"])
-                mark("conv")
-                q = ops.add_relu(y, e["c3"]["s_y"], e["c3"]["z_y"], idn, si, zi, so, zo, True)
-                mark("add")
-                yield
+            # conv3 + residual join in one launch
+            q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
+            mark("conv")
+            yield
             if keep:
                 inter[f"block{i}"] = q
         last = sp["blocks"][-1]["out"] if sp["blocks"] else (sp["stem"]["s_y"], sp["stem"]["z_y"])

@@ -138,37 +138,6 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
                           const float* vb, const float* multb, const int32_t* corrb, int y_zp,
                           int relub, const qcn_qdq_t* qdqb, int kmajor, uint8_t* y, void* stream);
 
-/* One 3x3 conv layer of qcn_conv3456_u8s8 (arguments as for
- * qcn_conv3x3_u8s8_nhwc; qdq may be NULL).  Its input zero point is the
- * previous layer's y_zp (or that layer's qdq->z2). */
-typedef struct qcn_conv_layer_t {
-  const int8_t* w_packed;
-  int cout;
-  const float* u;
-  const float* v;
-  const float* mult;
-  const int32_t* corr;
-  int y_zp;
-  int relu;
-  const qcn_qdq_t* qdq;
-} qcn_conv_layer_t;
-
-/* SimpleConvNet's second and third blocks in ONE launch: conv3(+ReLU) ->
- * conv4(+ReLU) -> max-pool -> conv5(+ReLU) -> conv6(+ReLU) -> max-pool
- * (baseline_model.py:20-34, :64-71; the int8 convs of StaticPTQModel /
- * CustomQuantizedSimpleConvNet).  Results equal qcn_conv3x3_pair_u8s8 for
- * conv3+conv4 followed by qcn_conv3x3_pair_u8s8 for conv5+conv6.
- *   x: u8 NHWC [nimg,16,16,64] (zero point x_zp); l3..l6 (host structs of
- *   device pointers): 64 -> 128 -> 128 -> 256 -> 256 channels;
- *   a4: device u8 NHWC [nimg,8,8,128], receives conv4's pooled output
- *   (scratch the launch reads back; valid afterwards);
- *   y: u8 NHWC [nimg,4,4,256], or chunk-major as qcn_conv3x3_u8s8_kmajor when
- *   kmajor != 0.  Other channel counts: QCN_ERR_UNSUPPORTED. */
-int qcn_conv3456_u8s8(const uint8_t* x, int nimg, int x_zp, const qcn_conv_layer_t* l3,
-                      const qcn_conv_layer_t* l4, const qcn_conv_layer_t* l5,
-                      const qcn_conv_layer_t* l6, uint8_t* a4, int kmajor, uint8_t* y,
-                      void* stream);
-
 /* A5/A6 as above, but y is written chunk-major for the classifier head:
  * y[f / 32][nimg][32] with f the NHWC flatten index of one image's output
  * (oh * ow * cout bytes).  Supported: the 8x8 layers with cout == 256
@@ -189,17 +158,16 @@ int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, i
 /* A9 x 2 + A7 — the static classifier head in two launches: fc1 (+ReLU)
  * u8 x s8 -> u8 [m, n1] as a 4-way split-K GEMM into an int32 workspace, then
  * one wave per row finishes fc1 (requant) and computes fc2 (n2 <= 16) and its
- * DeQuantStub (env QCN_FC_FUSED=1: one launch whose last-arriving workgroups
- * finish, through arrival counters in the workspace — slower, kept for A/B).  Same results as qcn_linear_u8s8(fc1) followed by
+ * DeQuantStub.  Same results as qcn_linear_u8s8(fc1) followed by
  * qcn_linear_u8s8(fc2, y_deq) — fc2's input zero point is y1_zp, fc2's
  * correction is applied exactly in the finisher (no corr2 argument).
  * x and w1 are CHUNK-MAJOR: x[k/32][m][32] (qcn_conv3x3_u8s8_kmajor writes
  * conv6's output that way), w1[k/32][n1][32] (qcn_pack_fc_kmajor).
  * corr1 = (128 - x_zp) * sum_k w1[f][k].  Supported: m % 128 == 0, n1 == 512,
- * k % 1024 == 0, n2 <= 16, m <= 65536 (QCN_ERR_UNSUPPORTED otherwise).  workspace: device
- * memory of qcn_classifier_workspace_size(m, n1) bytes, zero-filled before
- * its first use (every launch leaves its counters at zero); one workspace per
- * stream the head runs on concurrently. */
+ * k % 1024 == 0, n2 <= 16 (QCN_ERR_UNSUPPORTED otherwise).  workspace: device
+ * memory of qcn_classifier_workspace_size(m, n1) bytes (the int32 split-K
+ * partials; no initialisation needed); one workspace per stream the head runs
+ * on concurrently. */
 long long qcn_classifier_workspace_size(int m, int n1);
 /* Host: s8 [n][k] row-major -> [k/32][n][32] (k % 32 == 0). */
 int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out);

@@ -142,7 +142,7 @@ def test_config2_qdq_batch256_equals_torchao(dev, golden_dir):
     assert np.array_equal(logits2.cpu().numpy().argmax(1), z["argmax"])
 
 
-def test_qdq_head_equals_two_linears(dev, golden_dir, monkeypatch):
+def test_qdq_head_equals_two_linears(dev, golden_dir):
     """QDQ split-K head (fc1 int8 -> dequantize -> ReLU -> fp32 fc2 in the
     finisher) against the per-layer fc1 (linear_u8s8) + fp32 fc2
     (linear_f32) launches on the same conv6 output: fc1's u8 output
@@ -157,7 +157,7 @@ def test_qdq_head_equals_two_linears(dev, golden_dir, monkeypatch):
     assert model.kernel_names(x.shape)[-1] == "fc12"
     head = model.run(x).clone()
     f1_head = model.buffers(384)["f1"].clone()
-    monkeypatch.setenv("QCN_FC_HEAD", "linear")
+    model.fc_head = False
     assert model.kernel_names(x.shape)[-2:] == ("fc1", "fc2")
     lin = model.run(x).clone()
     torch.cuda.synchronize()

@@ -406,6 +406,43 @@ def test_classifier_head_repeated_full_batch(dev):
         assert torch.equal(y2f, y2f_ref)
 
 
+def test_classifier_head_above_65536_rows(dev):
+    """The head has no row limit beyond m % 128 == 0 (the workspace holds only
+    the split-K partials): 65664 rows run, and rows at both ends equal the two
+    static linear kernels bit for bit."""
+    from types import SimpleNamespace as NS
+    from qconvnet import ops, quant as Q
+    rng = np.random.default_rng(5)
+    m, k, n1, n2 = 65664, 4096, 512, 10
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    xk = torch.randint(0, 256, (k // 32, m, 32), dtype=torch.uint8, device=dev)
+    w1 = rng.integers(-128, 128, (n1, k), dtype=np.int8)
+    w2 = rng.integers(-128, 128, (n2, n1), dtype=np.int8)
+    s_x, s_y1, s_y2, s_w1, s_w2 = F32(0.02), F32(0.05), F32(0.11), F32(2e-4), F32(2e-3)
+    b1 = rng.normal(0, 0.5, n1).astype(F32)
+    b2 = rng.normal(0, 0.5, n2).astype(F32)
+    zx, z1, z2 = 7, 0, 100
+    u1, v1, m1 = Q.epilogue_constants(s_x, s_w1, s_y1, b1)
+    u2, v2, m2 = Q.epilogue_constants(s_y1, s_w2, s_y2, b2)
+    corr1 = ((128 - zx) * w1.astype(np.int64).sum(1)).astype(np.int32)
+    corr2 = ((128 - z1) * w2.astype(np.int64).sum(1)).astype(np.int32)
+    l1 = NS(w=T(w1), wk=T(ops.pack_fc_kmajor(w1)), u=T(u1), v=T(v1), mult=T(m1), corr=T(corr1),
+            z_y=z1, relu=True)
+    l2 = NS(w=T(w2), u=T(u2), v=T(v2), mult=T(m2), z_y=z2, relu=False, s_y=s_y2)
+    ws = ops.classifier_workspace(m, n1, dev)
+    y1 = torch.empty((m, n1), dtype=torch.uint8, device=dev)
+    y2 = torch.empty((m, n2), dtype=torch.uint8, device=dev)
+    y2f = torch.empty((m, n2), dtype=torch.float32, device=dev)
+    assert ops.classifier(xk, l1, l2, ws, y1, y2, y2f)
+    for sl in (slice(0, 128), slice(m - 128, m)):
+        x2 = ops.from_kmajor(xk[:, sl]).contiguous()
+        r1 = ops.linear_u8(x2, zx, T(w1), T(u1), T(v1), T(m1), T(corr1), z1, True)
+        r2, r2f = ops.linear_u8(r1, z1, T(w2), T(u2), T(v2), T(m2), T(corr2), z2, False,
+                                y_scale=s_y2, want_fp32=True)
+        torch.cuda.synchronize()
+        assert torch.equal(y1[sl], r1) and torch.equal(y2[sl], r2) and torch.equal(y2f[sl], r2f)
+
+
 @pytest.mark.parametrize("pool", [True, False])
 def test_conv_kmajor_output(dev, pool):
     """qcn_conv3x3_u8s8_kmajor writes exactly the NHWC result, chunk-major."""
@@ -429,24 +466,17 @@ def test_conv_kmajor_output(dev, pool):
     assert torch.equal(ops.from_kmajor(out), ref.view(n, -1))
 
 
-# the block launches under test: conv3..conv6 as ONE launch (qcn_conv3456_u8s8,
-# the default) or as the two pair launches (QCN_CONV3456=0)
-BLOCKS = [("1", "conv3456"), ("0", "conv34")]
-
-
-@pytest.mark.parametrize("block", BLOCKS, ids=["conv3456", "pairs"])
 @pytest.mark.parametrize("per_channel", [False, True])
-def test_conv_pairs_qdq_equal_layerwise(dev, per_channel, block, monkeypatch):
+def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
     """Same for the per-layer QDQ model (every qdq hand-off inside the fused
     launches)."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
-    monkeypatch.setenv("QCN_CONV3456", block[0])
     z = netfix.load(per_channel)
     spec = netfix.qdq_spec(z)
     x = torch.from_numpy(netfix.images(z)).to(dev)
     model = QuantizedConvNet(spec, dev)
-    assert block[1] in model.kernel_names(x.shape)
+    assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     a4_p = model.buffers(x.shape[0])["a4"].clone()
     model.fuse_pairs = False
@@ -456,24 +486,21 @@ def test_conv_pairs_qdq_equal_layerwise(dev, per_channel, block, monkeypatch):
     assert torch.equal(out_p, out_l)
 
 
-@pytest.mark.parametrize("block", BLOCKS, ids=["conv3456", "pairs"])
 @pytest.mark.parametrize("per_channel", [False, True])
-def test_conv_pairs_equal_layerwise(dev, per_channel, block, monkeypatch):
-    """conv3..conv6 as one launch, and conv3+conv4 / conv5+conv6 as two pair
-    launches (middle activations in LDS only), give the per-layer kernels'
-    outputs bit for bit — the conv4 output, the chunk-major conv6 output and
-    the logits — and the per-layer path itself matches the golden fixture
-    (test_full_net_*)."""
+def test_conv_pairs_equal_layerwise(dev, per_channel):
+    """conv3+conv4 / conv5+conv6 as two pair launches (middle activations in
+    LDS only) give the per-layer kernels' outputs bit for bit — the conv4
+    output, the chunk-major conv6 output and the logits — and the per-layer
+    path itself matches the golden fixture (test_full_net_*)."""
     import netfix
     from qconvnet import ops
     from qconvnet.qmodel import QuantizedConvNet
-    monkeypatch.setenv("QCN_CONV3456", block[0])
     z = netfix.load(per_channel)
     spec, _ = netfix.static_spec(z)
     x = torch.from_numpy(netfix.images(z)).to(dev)
     n = x.shape[0]
     model = QuantizedConvNet(spec, dev)
-    assert block[1] in model.kernel_names(x.shape)
+    assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     b = model.buffers(n)
     a4_p = b["a4"].clone()
@@ -489,30 +516,21 @@ def test_conv_pairs_equal_layerwise(dev, per_channel, block, monkeypatch):
     assert np.array_equal(out_p.cpu().numpy(), z["logits"])
 
 
-@pytest.mark.parametrize("impl", ["conv3456", "ga", "ring"])
-@pytest.mark.parametrize("n", [1, 6, 300, 1023, 1028])
-def test_conv56_pair_workgroup_shapes_equal_layerwise(dev, n, impl, monkeypatch):
-    """conv5+conv6 at batch sizes around the tilings: two images per 4-wave
-    workgroup (conv3456 and the weights-from-L2 pair "ga"; the last
-    workgroup holds one image when n is odd) and the LDS-ring pair ("ring":
-    two images per 4-wave workgroup below four images per CU, four per 8-wave
-    workgroup from 1024 on, 1028 a ragged last workgroup).  conv4's and
-    conv6's outputs and the logits equal the per-layer kernels' bit for bit."""
+@pytest.mark.parametrize("n", [1, 6, 255, 256, 257, 300, 513, 1023, 1028])
+def test_conv_pair_workgroup_shapes_equal_layerwise(dev, n):
+    """conv3+conv4 and conv5+conv6 at batch sizes around their tilings: at or
+    below one image per CU conv3+4 runs one image on 8 waves and conv5+6 splits
+    its output channels over two workgroups per image pair; above, conv3+4
+    runs one image per 4-wave workgroup and conv5+6 two images per 4-wave
+    workgroup (the last holds one image when n is odd).  conv4's and conv6's
+    outputs and the logits equal the per-layer kernels' bit for bit."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
     from oracle import torch_ref
-    monkeypatch.setenv("QCN_CONV3456", "1" if impl == "conv3456" else "0")
-    # QCN_PAIR56 is read once per process by the library: the ring case runs
-    # only when this process chose it
-    if impl == "ring" and os.environ.get("QCN_PAIR56", "4") != "0":
-        pytest.skip("the LDS-ring conv5+6 pair runs with QCN_PAIR56=0 set before the library loads")
-    if impl == "ga" and os.environ.get("QCN_PAIR56", "4") == "0":
-        pytest.skip("QCN_PAIR56=0 in this process")
     spec, _ = netfix.static_spec(netfix.load(False))
     x = torch.from_numpy(torch_ref.synthetic_images(n, 13)).to(dev)
     model = QuantizedConvNet(spec, dev)
-    assert model.kernel_names(x.shape)[1:3] == (("conv3456", "fc12" if n % 128 == 0 else "fc1")
-                                                if impl == "conv3456" else ("conv34", "conv56"))
+    assert model.kernel_names(x.shape)[1:3] == ("conv34", "conv56")
     out_p = model.run(x).clone()
     a4_p = model.buffers(n)["a4"].clone()
     a6_p = model.buffers(n)["a6"].clone()

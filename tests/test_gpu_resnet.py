@@ -365,6 +365,46 @@ def test_resnet_run_streams_equals_run(dev, nsplit):
     torch.cuda.synchronize()
 
 
+def test_resnet50_batch512_bench_path(dev):
+    """Config 5 at the batch it is benchmarked at: ResNet-50 224x224,
+    per-channel, batch 512, built exactly as bench.py --workload resnet50
+    builds it and run through the bench's own two-stream path
+    (run_streams(x, 2)).  Only at this size does the streaming 1x1 kernel walk
+    many 32-pixel strips per chunk with its counted-vmcnt prefetch (~196 per
+    chunk in layer 1, against 1 at batch 2).  Checks:
+      (a) run_streams(x, 2) == run(x) at 512, logits bit for bit;
+      (b) the static path is batch-independent, so every image's stem, block
+          and pooled u8 outputs and its logits at batch 512 equal the same
+          image run at batch 4 (128 small runs cover all 512 rows);
+      (c) a 2-image slice (the first and the last image) equals the numpy
+          oracle qref.resnet_int8_forward bit for bit, every block included.
+    Reference semantics: /root/reference/models/custom_quantization_model.py:79-143."""
+    from models.resnet import synthetic_images, synthetic_resnet
+    from qconvnet.resnet import quantize_resnet
+    fp = synthetic_resnet(0, device=dev, calib_images=32)
+    calib = [torch.from_numpy(synthetic_images(32, 1 + i)) for i in range(2)]
+    qm = quantize_resnet(fp, calib, dev, per_channel=True)
+    B = 512
+    xh = synthetic_images(B, 100)
+    x = torch.from_numpy(xh).to(dev)
+    out2 = qm.run_streams(x, 2).clone()
+    full, inter = qm.run(x, keep=True)
+    full = full.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(out2, full)
+    keys = ["stem", "pool"] + [f"block{i}" for i in range(len(qm.blocks))]
+    for i in range(0, B, 4):
+        o, it = qm.run(x[i:i + 4], keep=True)
+        assert torch.equal(o, full[i:i + 4]), i
+        for k in keys:
+            assert torch.equal(it[k], inter[k][i:i + 4]), (i, k)
+    idx = [0, B - 1]
+    ref, rinter = qref.resnet_int8_forward(xh[idx], qm.spec, keep=True)
+    for k in keys:
+        assert np.array_equal(inter[k][idx].cpu().numpy(), rinter[k]), k
+    assert np.array_equal(full[idx].cpu().numpy(), ref)
+
+
 def test_resnet_equals_torchao_fixture(dev):
     """§8(f)2 whole-net pin on the GPU: the 1-1-1-1 bottleneck ResNet at 64x64
     with torch.ao's qparams (tests/golden/net_resnet_int8.npz) — stem, every
