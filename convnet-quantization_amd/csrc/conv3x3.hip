@@ -25,6 +25,7 @@
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
 #include <type_traits>
+#include <utility>
 
 namespace qcn {
 
@@ -999,6 +1000,354 @@ void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
 }
 
 // --------------------------------------------------------------------------
+// conv3 + conv4 persistent and software-pipelined (batches above one image
+// per CU: the headline's batch 1024 gives four images per workgroup).
+//
+// One 4-wave workgroup per CU (one wave per SIMD, 512 registers each) loops
+// over its images.  Two accumulator sets per wave — X for conv3, Y for conv4 —
+// let one conv's epilogue run INSIDE the other conv's MFMA stream instead of
+// beside a co-resident workgroup that happens to be in another phase:
+//
+//   slot 1 of image j:  conv3(j)   -> X   | conv4's pooled epilogue of image
+//                                           j-2 from Y (requant, 16-B stores),
+//                                           image j+1 staged into the other
+//                                           conv3 patch buffer
+//   slot 2 of image j:  conv4(j-1) -> Y   | conv3's epilogue of image j from X
+//                                           (requant into the other conv4
+//                                           patch buffer)
+//
+// Each epilogue element (4 VALU: cvt, fma, mul, cvt_pk — FBGEMM-exact as
+// epilogue_tile_k) is placed after its own MFMA, at most one per two MFMAs,
+// so the VALU work issues in the MFMA pipe's shadow.  Weights stream from L2
+// into registers D K-steps ahead (as conv_mainloop_ga; D + 1 divides every
+// job's step count, so each job starts at register slot 0 and the last D
+// steps of a job prefetch the next job's first D).  With no LDS weight ring
+// the K loops have no barriers: two per image, at the slot boundaries.
+// The conv3 patch and the conv4 patch are double-buffered in LDS, their
+// zero-point halos written once per launch.
+template <class CA, class CB, int D>
+struct Pipe34 {
+  static_assert(CA::NWAVES == 4 && CB::NWAVES == 4 && CA::WCO == 2 && CB::WCO == 2 && CA::WI == 2 &&
+                CB::WI == 2 && CA::JT == 4 && CB::JT == 4, "four waves of 64-cout x 128-pixel tiles");
+  static_assert(!CA::kPool && CB::kPool && CA::kCout == CB::kCin && CA::kCout == CB::kCout, "A feeds B");
+  static_assert(CA::SEGS == 1 && CA::PXB == CA::IMG && CB::PXB == CB::IMG && CA::W == 16, "one image per tile");
+  static_assert(!CA::kSplit && CA::WBUF == CB::WBUF, "weight chunk stride shared by both convs");
+  static constexpr int SA = 2 * CA::NCH, SB = 2 * CB::NCH;   // K-steps per job
+  static_assert(SA % (D + 1) == 0 && SB % (D + 1) == 0, "every job starts at register slot 0");
+  static_assert(SA * 8 >= 144 && SB * 8 >= 256, "filler slots");
+  static constexpr int PA = (CA::PATCH + 15) / 16 * 16, PB = (CB::PATCH + 15) / 16 * 16;
+  static constexpr int OFF_PA = 0, OFF_PB = 2 * PA;
+  static constexpr int OFF_EA = OFF_PB + 2 * PB;           // u | v | mult, fp32 x cout each
+  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
+  static constexpr int OFF_CA = OFF_EB + 12 * CB::kCout;   // corr, int32 x cout
+  static constexpr int OFF_CB = OFF_CA + 4 * CA::kCout;
+  static constexpr int LDS = OFF_CB + 4 * CB::kCout;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+// Epilogue constants of 4 consecutive output channels from an LDS copy
+// (u | v | mult, cout floats each).
+struct EpiG {
+  float4 u, v, m;
+};
+QCN_DEV EpiG load_epig(const float* ek, int cout, int co) {
+  return {*reinterpret_cast<const float4*>(ek + co), *reinterpret_cast<const float4*>(ek + cout + co),
+          *reinterpret_cast<const float4*>(ek + 2 * cout + co)};
+}
+QCN_DEV float f4e(const float4& f, int e) { return e == 0 ? f.x : (e == 1 ? f.y : (e == 2 ? f.z : f.w)); }
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1 (a
+// guaranteed unroll, so every register-array index below is a constant).
+template <class F, int... I>
+QCN_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+QCN_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// One requantized output into byte e of wd (epilogue_tile_k's arithmetic).
+template <bool FAST>
+QCN_DEV uint32_t rq_elem(int a, const EpiG& K, int e, const ConvEpi& ep, uint32_t wd) {
+  const float u = f4e(K.u, e), v = f4e(K.v, e), m = f4e(K.m, e);
+  if constexpr (FAST) {
+    float f = __builtin_fmaf(u, v, (float)a);
+    f = f * m;
+    return __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
+  } else {
+    float q = requant_f(a, u, v, m, (float)ep.zp_y, (float)ep.lo);
+    if (ep.qdq) q = qdq_next_f(q, ep.s1, (float)ep.z1, ep.inv2, (float)ep.z2);
+    return __builtin_amdgcn_cvt_pk_u8_f32(q, e, wd);
+  }
+}
+
+// One conv of the pipeline over a staged patch: 2 * C::NCH K-steps of 8
+// MFMAs (64 couts x 128 pixels per wave), A fragments from registers (ga,
+// steps 0..D-1 already in flight), B fragments from the patch; fill(k) runs
+// after MFMA k.  Loads for the next job's first D steps come from wrn.
+template <class C, int D, class Fill>
+QCN_DEV void pipe_job(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_rsrc_t wrn, int voff, int wc,
+                      int wp, int l32, int hi, v16i (&acc)[2][4], v4i (&ga)[D + 1][2], Fill&& fill) {
+  constexpr int CBK = C::kCin / 64, S = 2 * C::NCH;
+  const PatchAddr<C> pa(wp, l32, hi);
+  v16i c0[2];   // the first K-step's C operand: the zero-point correction
+#pragma unroll
+  for (int i = 0; i < 2; ++i) c0[i] = acc_init_corr(corr, wc * 64 + i * 32, hi);
+  auto rd_b = [&](int s, int j) {
+    const int ch = s >> 1, kk = s & 1;
+    const int tap = ch / CBK, cb = ch % CBK;
+    return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 + kk * 32);
+  };
+  auto issue = [&](wt_rsrc_t r, int t, int slot) {
+    const int ch = t >> 1, kk = t & 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, ch * C::WBUF + i * 32 * 64 + kk * 32, 0);
+      ga[slot][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+    }
+  };
+  v4i fb[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = rd_b(0, j);
+  static_for<S>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<8>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      if constexpr (s + 1 < S && (m & 1) == 0) fb[(s + 1) & 1][m >> 1] = rd_b(s + 1, m >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[m >> 2][m & 3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ga[s % (D + 1)][m >> 2], fb[s & 1][m & 3],
+                                                                 s == 0 ? c0[m >> 2] : acc[m >> 2][m & 3], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (m == 3) {
+        // slot (s + D) % (D + 1) == (s - 1) % (D + 1): consumed by step s - 1
+        constexpr int t = s + D;
+        if constexpr (t < S) issue(wr, t, t % (D + 1));
+        else issue(wrn, t - S, t % (D + 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      fill(std::integral_constant<int, s * 8 + m>{});
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  });
+}
+
+// LDS writes of this wave complete, then the workgroup barrier (global stores
+// stay in flight: no vmcnt drain, unlike __syncthreads).
+QCN_DEV void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <class CA, class CB, int D, bool FA, bool FB>
+__global__ __launch_bounds__(256, 1)
+void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
+                    ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
+                    uint8_t* __restrict__ y) {
+  using P = Pipe34<CA, CB, D>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave & 1, wp = wave >> 1;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int b = (int)blockIdx.x, G = (int)gridDim.x;
+  const int T = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // this workgroup's images b, b + G, ...
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
+  int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
+  stage_epik<CA::kCout, 256>(epa, eka, tid);
+  stage_epik<CB::kCout, 256>(epb, ekb, tid);
+  if (tid < CA::kCout / 4) reinterpret_cast<int4*>(cra)[tid] = reinterpret_cast<const int4*>(epa.corr)[tid];
+  if (tid >= 64 && tid < 64 + CB::kCout / 4)
+    reinterpret_cast<int4*>(crb)[tid - 64] = reinterpret_cast<const int4*>(epb.corr)[tid - 64];
+  // zero-point halos of both buffers of both patches (never overwritten)
+  {
+    const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
+    constexpr int HS = 2 * 18 + 2 * 16;   // halo slots per patch
+    for (int e = tid; e < 2 * HS * (CA::kCin / 16); e += 256) {
+      const int bf = e / (HS * (CA::kCin / 16)), r = e % (HS * (CA::kCin / 16));
+      const int hs = r / (CA::kCin / 16), c = r % (CA::kCin / 16);
+      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
+      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
+      *reinterpret_cast<uint4*>(lds + P::OFF_PA + bf * P::PA + CA::slot(0, pr, pc) + c * 16) =
+          make_uint4(pa4, pa4, pa4, pa4);
+    }
+    for (int e = tid; e < 2 * HS * (CB::kCin / 16); e += 256) {
+      const int bf = e / (HS * (CB::kCin / 16)), r = e % (HS * (CB::kCin / 16));
+      const int hs = r / (CB::kCin / 16), c = r % (CB::kCin / 16);
+      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
+      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
+      *reinterpret_cast<uint4*>(lds + P::OFF_PB + bf * P::PB + CB::slot(0, pr, pc) + c * 16) =
+          make_uint4(pb4, pb4, pb4, pb4);
+    }
+  }
+  if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
+
+  // ---- per-lane addressing (lane-derived offsets that stay live)
+  const wt_rsrc_t wra = wt_rsrc(wa), wrb = wt_rsrc(wb);
+  const int voff = (wc * 64 + l32) * 64 + hi * 16;
+  // staging: the image is 16 KB contiguous; thread tid moves pieces tid + 256 q
+  // (pixel (tid >> 2) + 64 q: patch row (tid >> 6) + 4 q + 1, column ((tid >> 2) & 15) + 1)
+  const int st_dst = CA::slot(0, (tid >> 6) + 1, ((tid >> 2) & 15) + 1) + (tid & 3) * 16;
+
+  v16i accx[2][4], accy[2][4];
+  v4i ga[D + 1][2];
+  uint4 sv[4];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wra, voff, (t >> 1) * CA::WBUF + i * 2048 + (t & 1) * 32, 0);
+      ga[t][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+    }
+  }
+  {  // image b into conv3 patch buffer 0
+    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + tid * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<uint4*>(lds + P::OFF_PA + st_dst + q * 4 * CA::RS) =
+          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+  }
+  lds_barrier();
+
+  // Lane-derived values are recomputed from a laundered lane id in every
+  // slot: otherwise the loop-invariant LDS loads of the epilogue constants
+  // and corr tables are hoisted out of the image loop and held live across
+  // it (~250 registers, spilled).
+  struct Lane {
+    int l32, hi, ek, hb;
+    uint32_t yo;
+    const int *ca, *cb;
+  };
+  auto lanes = [&]() {
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    Lane L;
+    L.l32 = lz & 31;
+    L.hi = lz >> 5;
+    L.ek = wc * 64 + 4 * L.hi;
+    // conv3's epilogue into conv4's patch: tile (i, jj) pixel m = (4 wp + jj) 32 + l32
+    L.hb = CB::slot(0, wp * 8 + (L.l32 >> 4) + 1, (L.l32 & 15) + 1) + wc * 64 + 4 * L.hi;
+    // conv4's pooled output: pooled pixel wp * 32 + l32, 16 channels per lane after the swaps
+    L.yo = (uint32_t)((wp * 32 + L.l32) * CB::kCout + wc * 64 + 16 * L.hi);
+    L.ca = cra + (lz >> 6);   // (lz >> 6 == 0: an address the compiler cannot hoist)
+    L.cb = crb + (lz >> 6);
+    return L;
+  };
+  // ---- the fillers
+  // conv4's pooled epilogue from acc: element e (0..31) of the wave's two
+  // 32-channel tiles (max over the four quadrant tiles, requant); a tile's
+  // 16-B rows go out after its 16th element
+  EpiG kb;
+  uint32_t wq[4];
+  auto epi4 = [&](const Lane& L, v16i (&acc)[2][4], auto ec, wt_rsrc_t yr) {
+    constexpr int e = decltype(ec)::value;
+    constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3;
+    if constexpr (ee == 0) kb = load_epig(ekb, CB::kCout, L.ek + i * 32 + 8 * g);
+    const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
+    wq[g] = rq_elem<FB>(a, kb, ee, epb, ee == 0 ? 0u : wq[g]);
+    if constexpr (r == 15) {
+      auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
+      auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
+      uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
+      auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+      auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+      store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
+    }
+  };
+  // conv3's epilogue of accx into conv4 patch pb: element e (0..127), a dword
+  // to the patch after every fourth
+  EpiG ka;
+  uint32_t wd = 0;
+  auto epi3 = [&](const Lane& L, auto ec, uint8_t* pb) {
+    constexpr int e = decltype(ec)::value;
+    constexpr int i = e >> 6, jj = (e >> 4) & 3, r = e & 15, g = r >> 2, ee = r & 3;
+    if constexpr (ee == 0) ka = load_epig(eka, CA::kCout, L.ek + i * 32 + 8 * g);
+    wd = rq_elem<FA>(accx[i][jj][r], ka, ee, epa, ee == 0 ? 0u : wd);
+    if constexpr (ee == 3) *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
+  };
+  auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
+  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (j & 1) * P::PA; };
+  auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
+
+  // slot 1 of image j: conv3(j) -> accx | [conv4's epilogue of j - 2 from
+  // accy], staging of image j + 1 (a valid dummy past the last image)
+  auto slot1 = [&](int j, auto E4) {
+    const Lane L = lanes();
+    const wt_rsrc_t yr = img_out(decltype(E4)::value ? j - 2 : 0);
+    const int nn = j + 1 < T ? b + (j + 1) * G : b;
+    const uint8_t* src = x + (long)nn * CA::IMG * CA::kCin + tid * 16;
+    uint8_t* pdst = pa_buf(j + 1) + st_dst;
+    // the next job: conv4 of image j - 1, or conv3 of image 1 after image 0
+    const wt_rsrc_t wn = (j == 0 && T > 1) ? wra : wrb;
+    pipe_job<CA, D>(pa_buf(j), L.ca, wra, wn, voff, wc, wp, L.l32, L.hi, accx, ga, [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+      }
+      if constexpr (decltype(E4)::value && (k & 3) == 1 && (k >> 2) < 32)
+        epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
+      if constexpr (k >= 136 && k < 144 && (k & 1) == 0) {
+        constexpr int q = (k - 136) >> 1;
+        *reinterpret_cast<uint4*>(pdst + q * 4 * CA::RS) =
+            make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+      }
+    });
+    lds_barrier();
+  };
+  // slot 2 of image j: conv4(j - 1) -> accy | conv3's epilogue of image j
+  auto slot2 = [&](int j) {
+    const Lane L = lanes();
+    uint8_t* pb = pb_buf(j);
+    const wt_rsrc_t wn = j + 1 < T ? wra : wrb;   // next: conv3 of j + 1, or conv4 of j
+    pipe_job<CB, D>(pb_buf(j - 1), L.cb, wrb, wn, voff, wc, wp, L.l32, L.hi, accy, ga, [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr ((k & 1) == 1 && (k >> 1) < 128) epi3(L, std::integral_constant<int, (k >> 1)>{}, pb);
+    });
+    lds_barrier();
+  };
+
+  // image 0: conv3, then its epilogue on its own (nothing to overlap it with)
+  slot1(0, std::false_type{});
+  {
+    const Lane L = lanes();
+    uint8_t* pb0 = pb_buf(0);
+    static_for<128>([&](auto ec) { epi3(L, ec, pb0); });
+    lds_barrier();
+  }
+  if (T > 1) {
+    slot1(1, std::false_type{});
+    slot2(1);
+  }
+#pragma unroll 1
+  for (int j = 2; j < T; ++j) {
+    slot1(j, std::true_type{});
+    slot2(j);
+  }
+  // conv4 of the last image into accx (free since its conv3 epilogue) with
+  // conv4's epilogue of image T - 2 from accy as filler (T == 1: accy holds
+  // nothing; that garbage goes to image b's output and is overwritten by the
+  // real epilogue below, later in this wave's program order)
+  {
+    const Lane L = lanes();
+    const wt_rsrc_t yr = img_out(T >= 2 ? T - 2 : 0);
+    pipe_job<CB, D>(pb_buf(T - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, accx, ga, [&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr ((k & 3) == 1 && (k >> 2) < 32) epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
+    });
+    const Lane L2 = lanes();
+    const wt_rsrc_t yl = img_out(T - 1);
+    static_for<32>([&](auto ec) { epi4(L2, accx, ec, yl); });
+  }
+}
+
+// --------------------------------------------------------------------------
 // conv1: CIN = 3, input fp32 NCHW quantized on the fly (aten quantize_per_tensor
 // semantics, oracle qref A1), im2col rows of K = 27 (+5 zero) bytes in LDS,
 // one 32x32x32 MFMA k-step.  HBM-bound layer (52 op/B).
@@ -1663,6 +2012,30 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+template <class CA, class CB, int D, bool FA, bool FB>
+int launch_pipe34_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
+                    const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
+  using P = Pipe34<CA, CB, D>;
+  auto k = conv34p_kernel<CA, CB, D, FA, FB>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  const int grid = nimg < ncu ? nimg : ncu;   // persistent: one workgroup per CU
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+template <class CA, class CB, int D>
+int launch_pipe34(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
+                  const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
+  // the FBGEMM fast path (zp_y == 0, no floor, no QDQ hand-off) is known on the host
+  const bool fa = epa.zp_y == 0 && epa.lo == 0 && epa.qdq == 0;
+  const bool fb = epb.zp_y == 0 && epb.lo == 0 && epb.qdq == 0;
+  if (fa && fb) return launch_pipe34_k<CA, CB, D, true, true>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+  if (fa) return launch_pipe34_k<CA, CB, D, true, false>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+  if (fb) return launch_pipe34_k<CA, CB, D, false, true>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+  return launch_pipe34_k<CA, CB, D, false, false>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+}
+
 template <class CA, class CB, int D, int COUTB>
 int launch_pair_ga_split(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa,
                          int xb_zp, const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st) {
@@ -1803,9 +2176,11 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
       return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    return launch_pair<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
-                       ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
-        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
+    using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+    // above one image per CU: the persistent software-pipelined kernel
+    if (!kmajor) return launch_pipe34<A3, B4, 5>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
+    return launch_pair<A3, B4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
     // two images per 4-wave workgroup, two workgroups per CU, weights from L2
