@@ -27,6 +27,12 @@
 #include <type_traits>
 #include <utility>
 
+// weight-prefetch depth (K-steps) of the pipelined conv3+conv4 kernel; D + 1
+// must divide 18 (build-time constant, not a runtime switch)
+#ifndef QCN_PIPE34_D
+#define QCN_PIPE34_D 5
+#endif
+
 namespace qcn {
 
 // conv12 producer waves' issue priority (swept: 1-3 within noise, 2 best;
@@ -1243,14 +1249,19 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
   // conv4's pooled epilogue from acc: element e (0..31) of the wave's two
   // 32-channel tiles (max over the four quadrant tiles, requant); a tile's
   // 16-B rows go out after its 16th element
-  EpiG kb;
+  // The constants of each 4-channel group are read from LDS one group ahead
+  // (double-buffered): read right before use, each group's first element
+  // waited on the LDS round trip.
+  EpiG kb[2];
   uint32_t wq[4];
+  auto epi4_pre = [&](const Lane& L) { kb[0] = load_epig(ekb, CB::kCout, L.ek); };
   auto epi4 = [&](const Lane& L, v16i (&acc)[2][4], auto ec, wt_rsrc_t yr) {
     constexpr int e = decltype(ec)::value;
-    constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3;
-    if constexpr (ee == 0) kb = load_epig(ekb, CB::kCout, L.ek + i * 32 + 8 * g);
+    constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3, gg = e >> 2;
+    if constexpr (ee == 0 && gg + 1 < 8)
+      kb[(gg + 1) & 1] = load_epig(ekb, CB::kCout, L.ek + ((gg + 1) >> 2) * 32 + 8 * ((gg + 1) & 3));
     const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
-    wq[g] = rq_elem<FB>(a, kb, ee, epb, ee == 0 ? 0u : wq[g]);
+    wq[g] = rq_elem<FB>(a, kb[gg & 1], ee, epb, ee == 0 ? 0u : wq[g]);
     if constexpr (r == 15) {
       auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
       auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
@@ -1262,13 +1273,16 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
   };
   // conv3's epilogue of accx into conv4 patch pb: element e (0..127), a dword
   // to the patch after every fourth
-  EpiG ka;
+  EpiG ka[2];
   uint32_t wd = 0;
+  auto epi3_pre = [&](const Lane& L) { ka[0] = load_epig(eka, CA::kCout, L.ek); };
   auto epi3 = [&](const Lane& L, auto ec, uint8_t* pb) {
     constexpr int e = decltype(ec)::value;
     constexpr int i = e >> 6, jj = (e >> 4) & 3, r = e & 15, g = r >> 2, ee = r & 3;
-    if constexpr (ee == 0) ka = load_epig(eka, CA::kCout, L.ek + i * 32 + 8 * g);
-    wd = rq_elem<FA>(accx[i][jj][r], ka, ee, epa, ee == 0 ? 0u : wd);
+    // group order: (i, jj, g); the constants depend on (i, g) only
+    constexpr int gg = e >> 2, gn = gg + 1, in = gn >> 4, g_n = gn & 3;
+    if constexpr (ee == 0 && gn < 32) ka[gn & 1] = load_epig(eka, CA::kCout, L.ek + in * 32 + 8 * g_n);
+    wd = rq_elem<FA>(accx[i][jj][r], ka[gg & 1], ee, epa, ee == 0 ? 0u : wd);
     if constexpr (ee == 3) *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
   };
   auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
@@ -1290,6 +1304,7 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
       if constexpr (k == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+        if constexpr (decltype(E4)::value) epi4_pre(L);
       }
       if constexpr (decltype(E4)::value && (k & 3) == 1 && (k >> 2) < 32)
         epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
@@ -1308,6 +1323,7 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
     const wt_rsrc_t wn = j + 1 < T ? wra : wrb;   // next: conv3 of j + 1, or conv4 of j
     pipe_job<CB, D>(pb_buf(j - 1), L.cb, wrb, wn, voff, wc, wp, L.l32, L.hi, accy, ga, [&](auto kc) {
       constexpr int k = decltype(kc)::value;
+      if constexpr (k == 0) epi3_pre(L);
       if constexpr ((k & 1) == 1 && (k >> 1) < 128) epi3(L, std::integral_constant<int, (k >> 1)>{}, pb);
     });
     lds_barrier();
@@ -1318,6 +1334,7 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
   {
     const Lane L = lanes();
     uint8_t* pb0 = pb_buf(0);
+    epi3_pre(L);
     static_for<128>([&](auto ec) { epi3(L, ec, pb0); });
     lds_barrier();
   }
@@ -1339,10 +1356,12 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
     const wt_rsrc_t yr = img_out(T >= 2 ? T - 2 : 0);
     pipe_job<CB, D>(pb_buf(T - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, accx, ga, [&](auto kc) {
       constexpr int k = decltype(kc)::value;
+      if constexpr (k == 0) epi4_pre(L);
       if constexpr ((k & 3) == 1 && (k >> 2) < 32) epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
     });
     const Lane L2 = lanes();
     const wt_rsrc_t yl = img_out(T - 1);
+    epi4_pre(L2);
     static_for<32>([&](auto ec) { epi4(L2, accx, ec, yl); });
   }
 }
@@ -2179,7 +2198,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
     using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
     // above one image per CU: the persistent software-pipelined kernel
-    if (!kmajor) return launch_pipe34<A3, B4, 5>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
+    if (!kmajor) return launch_pipe34<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
     return launch_pair<A3, B4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
