@@ -30,7 +30,7 @@
 // weight-prefetch depth (K-steps) of the pipelined conv3+conv4 kernel; D + 1
 // must divide 18 (build-time constant, not a runtime switch)
 #ifndef QCN_PIPE34_D
-#define QCN_PIPE34_D 5
+#define QCN_PIPE34_D 2
 #endif
 
 namespace qcn {
@@ -1092,7 +1092,7 @@ QCN_DEV uint32_t rq_elem(int a, const EpiG& K, int e, const ConvEpi& ep, uint32_
 // MFMAs (64 couts x 128 pixels per wave), A fragments from registers (ga,
 // steps 0..D-1 already in flight), B fragments from the patch; fill(k) runs
 // after MFMA k.  Loads for the next job's first D steps come from wrn.
-template <class C, int D, class Fill>
+template <class C, int D, bool PIN = false, class Fill>
 QCN_DEV void pipe_job(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_rsrc_t wrn, int voff, int wc,
                       int wp, int l32, int hi, v16i (&acc)[2][4], v4i (&ga)[D + 1][2], Fill&& fill) {
   constexpr int CBK = C::kCin / 64, S = 2 * C::NCH;
@@ -1135,8 +1135,36 @@ QCN_DEV void pipe_job(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_rs
       fill(std::integral_constant<int, s * 8 + m>{});
       __builtin_amdgcn_sched_barrier(0);
     });
+    // pin the step's MFMAs here (as conv_mainloop): side-effect free, they
+    // could otherwise be sunk towards their uses and the fragment registers
+    // held live (spilled) across the loop.  Only for accumulators that live
+    // in VGPRs (two waves per SIMD): the pin would copy AGPR accumulators.
+    if constexpr (PIN) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]));
+    }
   });
 }
+
+#ifdef QCN_PIPE34_STAMP
+// Diagnostic builds only (tools/build_variant.sh): per-workgroup s_memtime
+// stamps of wave 0 around every pipeline barrier, [wg][stamp]; plain vector
+// stores into a buffer nothing else reads.
+__device__ unsigned long long g_p34_stamp[1024][64];
+QCN_DEV void p34_stamp(int& idx, unsigned long long t) {
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (threadIdx.x < 64 && lane == 0 && blockIdx.x < 1024 && idx < 64) {
+    volatile unsigned long long* d = &g_p34_stamp[blockIdx.x][idx];
+    *d = t + lane;
+  }
+  ++idx;
+}
+#define P34_STAMP() p34_stamp(stamp_i, __builtin_amdgcn_s_memtime())
+#else
+#define P34_STAMP()
+#endif
 
 // LDS writes of this wave complete, then the workgroup barrier (global stores
 // stay in flight: no vmcnt drain, unlike __syncthreads).
@@ -1160,6 +1188,14 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
   const int l32 = lane & 31, hi = lane >> 5;
   const int b = (int)blockIdx.x, G = (int)gridDim.x;
   const int T = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // this workgroup's images b, b + G, ...
+#ifdef QCN_PIPE34_STAMP
+  int stamp_i = 0;
+  if (threadIdx.x < 64) {
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    p34_stamp(stamp_i, r0);
+  }
+#endif
+  P34_STAMP();
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
   int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
@@ -1219,7 +1255,9 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
       *reinterpret_cast<uint4*>(lds + P::OFF_PA + st_dst + q * 4 * CA::RS) =
           make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
   }
+  P34_STAMP();
   lds_barrier();
+  P34_STAMP();
 
   // Lane-derived values are recomputed from a laundered lane id in every
   // slot: otherwise the loop-invariant LDS loads of the epilogue constants
@@ -1314,7 +1352,9 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
             make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
       }
     });
+    P34_STAMP();
     lds_barrier();
+    P34_STAMP();
   };
   // slot 2 of image j: conv4(j - 1) -> accy | conv3's epilogue of image j
   auto slot2 = [&](int j) {
@@ -1326,7 +1366,9 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
       if constexpr (k == 0) epi3_pre(L);
       if constexpr ((k & 1) == 1 && (k >> 1) < 128) epi3(L, std::integral_constant<int, (k >> 1)>{}, pb);
     });
+    P34_STAMP();
     lds_barrier();
+    P34_STAMP();
   };
 
   // image 0: conv3, then its epilogue on its own (nothing to overlap it with)
@@ -1336,7 +1378,9 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
     uint8_t* pb0 = pb_buf(0);
     epi3_pre(L);
     static_for<128>([&](auto ec) { epi3(L, ec, pb0); });
+    P34_STAMP();
     lds_barrier();
+    P34_STAMP();
   }
   if (T > 1) {
     slot1(1, std::false_type{});
@@ -1364,6 +1408,223 @@ void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int
     epi4_pre(L2);
     static_for<32>([&](auto ec) { epi4(L2, accx, ec, yl); });
   }
+  P34_STAMP();
+#ifdef QCN_PIPE34_STAMP
+  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
+#endif
+}
+
+
+// --------------------------------------------------------------------------
+// conv3 + conv4 with wave-specialised roles (persistent; above one image per
+// CU).  One 8-wave workgroup per CU: waves 0-3 run conv3, waves 4-7 conv4,
+// so every SIMD holds one wave of each role (a workgroup's waves go to the
+// SIMDs cyclically).  In period p (one workgroup barrier per period):
+//
+//   conv3 waves:  conv3(p) -> acc, then conv3's epilogue of image p into the
+//                 conv4 patch buffer p & 1, and image p + 1 staged into the
+//                 conv3 patch buffer (p + 1) & 1 (loads issued before the
+//                 epilogue, written after it);
+//   conv4 waves:  conv4's pooled epilogue of image p - 2 (acc), then
+//                 conv4(p - 1) -> acc from the conv4 patch buffer (p - 1) & 1.
+//
+// Each role's VALU epilogue runs beside the other role's MFMAs on the same
+// SIMD, at a fixed phase (conv4's at the period start, conv3's at its end),
+// instead of wherever two independent workgroups happen to drift.  Weights
+// stream from L2 into registers D K-steps ahead; the last D steps of a job
+// prefetch the next period's first D.  LDS: both patches double-buffered
+// (halos written once per launch), epilogue constants and corr tables.
+template <class CA, class CB, int D, bool FA, bool FB>
+__global__ __launch_bounds__(512, 1)
+void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
+                     ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
+                     uint8_t* __restrict__ y) {
+  using P = Pipe34<CA, CB, D>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+  const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // 0: conv3, 1: conv4
+  const int rt = tid & 255, lane = tid & 63, wave = rt >> 6;   // thread / wave within the role
+  const int wc = wave & 1, wp = wave >> 1;
+  const int b = (int)blockIdx.x, G = (int)gridDim.x;
+  const int T = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // this workgroup's images b, b + G, ...
+#ifdef QCN_PIPE34_STAMP
+  int stamp_i = 0;
+  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
+#endif
+  P34_STAMP();
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
+  int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
+  stage_epik<CA::kCout, 512>(epa, eka, tid);
+  stage_epik<CB::kCout, 512>(epb, ekb, tid);
+  if (tid < CA::kCout / 4) reinterpret_cast<int4*>(cra)[tid] = reinterpret_cast<const int4*>(epa.corr)[tid];
+  if (tid >= 64 && tid < 64 + CB::kCout / 4)
+    reinterpret_cast<int4*>(crb)[tid - 64] = reinterpret_cast<const int4*>(epb.corr)[tid - 64];
+  {  // zero-point halos of both buffers of both patches (never overwritten)
+    const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
+    constexpr int HS = 2 * 18 + 2 * 16;   // halo slots per patch
+    for (int e = tid; e < 2 * HS * (CA::kCin / 16); e += 512) {
+      const int bf = e / (HS * (CA::kCin / 16)), r = e % (HS * (CA::kCin / 16));
+      const int hs = r / (CA::kCin / 16), c = r % (CA::kCin / 16);
+      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
+      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
+      *reinterpret_cast<uint4*>(lds + P::OFF_PA + bf * P::PA + CA::slot(0, pr, pc) + c * 16) =
+          make_uint4(pa4, pa4, pa4, pa4);
+    }
+    for (int e = tid; e < 2 * HS * (CB::kCin / 16); e += 512) {
+      const int bf = e / (HS * (CB::kCin / 16)), r = e % (HS * (CB::kCin / 16));
+      const int hs = r / (CB::kCin / 16), c = r % (CB::kCin / 16);
+      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
+      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
+      *reinterpret_cast<uint4*>(lds + P::OFF_PB + bf * P::PB + CB::slot(0, pr, pc) + c * 16) =
+          make_uint4(pb4, pb4, pb4, pb4);
+    }
+  }
+  if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
+
+  const int l32 = lane & 31, hi = lane >> 5;
+  const wt_rsrc_t wra = wt_rsrc(wa), wrb = wt_rsrc(wb);
+  const int voff = (wc * 64 + l32) * 64 + hi * 16;
+  // staging (conv3 waves): the image is 16 KB contiguous; role thread rt moves
+  // pieces rt + 256 q (patch row (rt >> 6) + 4 q + 1, column ((rt >> 2) & 15) + 1)
+  const int st_dst = CA::slot(0, (rt >> 6) + 1, ((rt >> 2) & 15) + 1) + (rt & 3) * 16;
+  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (j & 1) * P::PA; };
+  auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
+
+  v16i acc[2][4];
+  v4i ga[D + 1][2];
+  {
+    const wt_rsrc_t w0 = role == 0 ? wra : wrb;
+#pragma unroll
+    for (int t = 0; t < D; ++t) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(w0, voff, (t >> 1) * CA::WBUF + i * 2048 + (t & 1) * 32, 0);
+        ga[t][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+      }
+    }
+  }
+  uint4 sv[4];
+  if (role == 0) {  // image b into conv3 patch buffer 0
+    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + rt * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<uint4*>(pa_buf(0) + st_dst + q * 4 * CA::RS) =
+          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+  }
+  P34_STAMP();
+  lds_barrier();
+  P34_STAMP();
+
+  // lane-derived epilogue addressing from a laundered lane id (not hoisted
+  // out of the period loop and held live across the MFMA jobs)
+  struct Lane {
+    int l32, hi, ek, hb;
+    uint32_t yo;
+    const int *ca, *cb;
+  };
+  auto lanes = [&]() {
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    Lane L;
+    L.l32 = lz & 31;
+    L.hi = lz >> 5;
+    L.ek = wc * 64 + 4 * L.hi;
+    L.hb = CB::slot(0, wp * 8 + (L.l32 >> 4) + 1, (L.l32 & 15) + 1) + wc * 64 + 4 * L.hi;
+    L.yo = (uint32_t)((wp * 32 + L.l32) * CB::kCout + wc * 64 + 16 * L.hi);
+    L.ca = cra + (lz >> 6);
+    L.cb = crb + (lz >> 6);
+    return L;
+  };
+  // conv3's epilogue of acc into conv4 patch pb (epilogue_tile_k's numerics;
+  // each 4-channel group's constants read one group ahead)
+  auto epi3 = [&](const Lane& L, uint8_t* pb) {
+    EpiG ka[2];
+    uint32_t wd = 0;
+    ka[0] = load_epig(eka, CA::kCout, L.ek);
+    static_for<128>([&](auto ec) {
+      constexpr int e = decltype(ec)::value;
+      constexpr int i = e >> 6, jj = (e >> 4) & 3, r = e & 15, g = r >> 2, ee = r & 3;
+      constexpr int gg = e >> 2, gn = gg + 1;
+      if constexpr (ee == 0 && gn < 32)
+        ka[gn & 1] = load_epig(eka, CA::kCout, L.ek + (gn >> 4) * 32 + 8 * (gn & 3));
+      wd = rq_elem<FA>(acc[i][jj][r], ka[gg & 1], ee, epa, ee == 0 ? 0u : wd);
+      if constexpr (ee == 3)
+        *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
+    });
+  };
+  // conv4's pooled epilogue of acc (max over the four quadrant tiles, requant,
+  // two permlane32 swap rounds, one 16-B store per tile and lane)
+  auto epi4 = [&](const Lane& L, wt_rsrc_t yr) {
+    EpiG kb[2];
+    uint32_t wq[4];
+    kb[0] = load_epig(ekb, CB::kCout, L.ek);
+    static_for<32>([&](auto ec) {
+      constexpr int e = decltype(ec)::value;
+      constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3, gg = e >> 2;
+      if constexpr (ee == 0 && gg + 1 < 8)
+        kb[(gg + 1) & 1] = load_epig(ekb, CB::kCout, L.ek + ((gg + 1) >> 2) * 32 + 8 * ((gg + 1) & 3));
+      const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
+      wq[g] = rq_elem<FB>(a, kb[gg & 1], ee, epb, ee == 0 ? 0u : wq[g]);
+      if constexpr (r == 15) {
+        auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
+        auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
+        uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
+        auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+        auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+        store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
+      }
+    });
+  };
+  auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
+  auto nofill = [](auto) {};
+
+  // Each role runs its own period loop (T + 1 periods, one barrier each, so
+  // the two roles pass the same barriers).
+  if (role == 0) {
+#pragma unroll 1
+    for (int p = 0; p <= T; ++p) {
+      if (p < T) {
+        const Lane L = lanes();
+        pipe_job<CA, D, true>(pa_buf(p), L.ca, wra, wra, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
+        // image p + 1 (a valid dummy past the last): loads now, written after the epilogue
+        const int nn = p + 1 < T ? b + (p + 1) * G : b;
+        const uint8_t* src = x + (long)nn * CA::IMG * CA::kCin + rt * 16;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+        epi3(L, pb_buf(p));
+        uint8_t* pdst = pa_buf(p + 1) + st_dst;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<uint4*>(pdst + q * 4 * CA::RS) =
+              make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+      }
+      P34_STAMP();
+      lds_barrier();
+      P34_STAMP();
+    }
+  } else {
+#pragma unroll 1
+    for (int p = 0; p <= T; ++p) {
+      if (p >= 1) {
+        const Lane L = lanes();
+        if (p >= 2) epi4(L, img_out(p - 2));
+        pipe_job<CB, D, true>(pb_buf(p - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
+      }
+      P34_STAMP();
+      lds_barrier();
+      P34_STAMP();
+    }
+    const Lane L = lanes();
+    epi4(L, img_out(T - 1));
+  }
+  P34_STAMP();
+#ifdef QCN_PIPE34_STAMP
+  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // --------------------------------------------------------------------------
@@ -2031,15 +2292,19 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+#ifndef QCN_CONV34_WS
+#define QCN_CONV34_WS 1
+#endif
 template <class CA, class CB, int D, bool FA, bool FB>
 int launch_pipe34_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
                     const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
   using P = Pipe34<CA, CB, D>;
-  auto k = conv34p_kernel<CA, CB, D, FA, FB>;
+  auto k = QCN_CONV34_WS ? conv34ws_kernel<CA, CB, D, FA, FB> : conv34p_kernel<CA, CB, D, FA, FB>;
   static bool attr_done[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
   const int grid = nimg < ncu ? nimg : ncu;   // persistent: one workgroup per CU
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(QCN_CONV34_WS ? 512 : 256), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp,
+                     wb, epb, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
@@ -2106,6 +2371,14 @@ int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nim
 }  // namespace
 
 extern "C" {
+
+#ifdef QCN_PIPE34_STAMP
+int qcn_diag_p34_stamps(unsigned long long* host, int nwg) {
+  if (!host || nwg <= 0 || nwg > 1024) return QCN_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_p34_stamp), (size_t)nwg * 64 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+#endif
 
 int qcn_conv3x3_packed_size(int cin, int cout) { return 9 * cin * cout; }
 
