@@ -1452,6 +1452,14 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
   if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
   P34_STAMP();
+  // image b's conv3 input (conv3 waves): loads first, so their latency runs
+  // under the table / halo set-up below
+  uint4 sv[4];
+  if (role == 0 && b < nimg) {
+    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + (tid & 255) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+  }
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
   int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
@@ -1505,11 +1513,7 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
       }
     }
   }
-  uint4 sv[4];
   if (role == 0) {  // image b into conv3 patch buffer 0
-    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + rt * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<uint4*>(pa_buf(0) + st_dst + q * 4 * CA::RS) =
@@ -1539,44 +1543,50 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
     L.cb = crb + (lz >> 6);
     return L;
   };
-  // conv3's epilogue of acc into conv4 patch pb (epilogue_tile_k's numerics;
-  // each 4-channel group's constants read one group ahead)
+  // conv3's epilogue of acc into conv4 patch pb (epilogue_tile_k's numerics).
+  // The constants of a 32-channel tile row (4 groups of 4 channels) are read
+  // from LDS together: one LDS round trip per tile row.
   auto epi3 = [&](const Lane& L, uint8_t* pb) {
-    EpiG ka[2];
-    uint32_t wd = 0;
-    ka[0] = load_epig(eka, CA::kCout, L.ek);
-    static_for<128>([&](auto ec) {
-      constexpr int e = decltype(ec)::value;
-      constexpr int i = e >> 6, jj = (e >> 4) & 3, r = e & 15, g = r >> 2, ee = r & 3;
-      constexpr int gg = e >> 2, gn = gg + 1;
-      if constexpr (ee == 0 && gn < 32)
-        ka[gn & 1] = load_epig(eka, CA::kCout, L.ek + (gn >> 4) * 32 + 8 * (gn & 3));
-      wd = rq_elem<FA>(acc[i][jj][r], ka[gg & 1], ee, epa, ee == 0 ? 0u : wd);
-      if constexpr (ee == 3)
+    static_for<2>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      EpiG K[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) K[g] = load_epig(eka, CA::kCout, L.ek + i * 32 + 8 * g);
+      static_for<16>([&](auto qc) {   // (tile jj, group g): one dword of 4 channels
+        constexpr int jj = decltype(qc)::value >> 2, g = decltype(qc)::value & 3;
+        uint32_t wd = 0;
+#pragma unroll
+        for (int ee = 0; ee < 4; ++ee) wd = rq_elem<FA>(acc[i][jj][4 * g + ee], K[g], ee, epa, wd);
         *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
+      });
     });
   };
   // conv4's pooled epilogue of acc (max over the four quadrant tiles, requant,
   // two permlane32 swap rounds, one 16-B store per tile and lane)
   auto epi4 = [&](const Lane& L, wt_rsrc_t yr) {
-    EpiG kb[2];
-    uint32_t wq[4];
-    kb[0] = load_epig(ekb, CB::kCout, L.ek);
-    static_for<32>([&](auto ec) {
-      constexpr int e = decltype(ec)::value;
-      constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3, gg = e >> 2;
-      if constexpr (ee == 0 && gg + 1 < 8)
-        kb[(gg + 1) & 1] = load_epig(ekb, CB::kCout, L.ek + ((gg + 1) >> 2) * 32 + 8 * ((gg + 1) & 3));
-      const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
-      wq[g] = rq_elem<FB>(a, kb[gg & 1], ee, epb, ee == 0 ? 0u : wq[g]);
-      if constexpr (r == 15) {
-        auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
-        auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
-        uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
-        auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
-        auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
-        store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
+    static_for<2>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      EpiG K[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) K[g] = load_epig(ekb, CB::kCout, L.ek + i * 32 + 8 * g);
+      uint32_t wq[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int ee = 0; ee < 4; ++ee) {
+          const int r = 4 * g + ee;
+          const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
+          wd = rq_elem<FB>(a, K[g], ee, epb, wd);
+        }
+        wq[g] = wd;
       }
+      auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
+      auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
+      uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
+      auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+      auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+      store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
     });
   };
   auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
