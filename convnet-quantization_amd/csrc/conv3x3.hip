@@ -1464,11 +1464,29 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
   int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
   int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
-  stage_epik<CA::kCout, 512>(epa, eka, tid);
-  stage_epik<CB::kCout, 512>(epb, ekb, tid);
-  if (tid < CA::kCout / 4) reinterpret_cast<int4*>(cra)[tid] = reinterpret_cast<const int4*>(epa.corr)[tid];
-  if (tid >= 64 && tid < 64 + CB::kCout / 4)
-    reinterpret_cast<int4*>(crb)[tid - 64] = reinterpret_cast<const int4*>(epb.corr)[tid - 64];
+  // the epilogue tables (u | v | mult of both convs, both corr): one 16-B
+  // piece per conv4-role thread, loaded now and written after the halos
+  static_assert(CA::kCout == 128 && CB::kCout == 128, "table split below");
+  const int tt = tid - 256;   // 0..255 in the conv4 role
+  const float4* tsrc = nullptr;
+  float4* tdst = nullptr;
+  if (role == 1) {
+    if (tt < 96) {
+      tsrc = reinterpret_cast<const float4*>(tt < 32 ? epa.u : tt < 64 ? epa.v : epa.mult) + (tt & 31);
+      tdst = reinterpret_cast<float4*>(eka) + tt;
+    } else if (tt < 192) {
+      const int t2 = tt - 96;
+      tsrc = reinterpret_cast<const float4*>(t2 < 32 ? epb.u : t2 < 64 ? epb.v : epb.mult) + (t2 & 31);
+      tdst = reinterpret_cast<float4*>(ekb) + t2;
+    } else if (tt < 224) {
+      tsrc = reinterpret_cast<const float4*>(epa.corr) + (tt - 192);
+      tdst = reinterpret_cast<float4*>(cra) + (tt - 192);
+    } else {
+      tsrc = reinterpret_cast<const float4*>(epb.corr) + (tt - 224);
+      tdst = reinterpret_cast<float4*>(crb) + (tt - 224);
+    }
+  }
+  const float4 tval = role == 1 ? *tsrc : make_float4(0.f, 0.f, 0.f, 0.f);
   {  // zero-point halos of both buffers of both patches (never overwritten)
     const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
     constexpr int HS = 2 * 18 + 2 * 16;   // halo slots per patch
@@ -1489,6 +1507,7 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
           make_uint4(pb4, pb4, pb4, pb4);
     }
   }
+  if (role == 1) *tdst = tval;
   if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
 
   const int l32 = lane & 31, hi = lane >> 5;

@@ -12,6 +12,8 @@
 // buffer of their own that nothing else reads).  Linked with the product's
 // other objects into libqconvnet_clock.so and loaded via QCN_LIB by
 // tools/clock_probe.py; the product library never contains a stamp.
+// the pipelined conv3+conv4 kernel's own stamps (g_p34_stamp) are compiled in
+#define QCN_PIPE34_STAMP 1
 #define qcn_conv3x3_pair_u8s8 qcn_conv3x3_pair_u8s8__product
 #define qcn_conv12_fused_f32_nchw qcn_conv12_fused_f32_nchw__product
 #include "conv3x3.hip"
@@ -115,6 +117,8 @@ int launch_pair_ga_stamped(int kind, const uint8_t* x, int nimg, int x_zp, const
 }  // namespace
 }  // namespace qcn
 
+static bool g_last34_ws = false;   // the last conv3+conv4 launch was the pipelined kernel
+
 extern "C" {
 
 // Same signature and shape dispatch as the product's qcn_conv3x3_pair_u8s8.
@@ -143,13 +147,15 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   const int ncu = qcn_cu_count();
   const bool small = ncu > 0 && nimg <= ncu;
   if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
+    g_last34_ws = !small && !kmajor;
     if (small)
       return launch_pair_stamped<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                                  ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    return launch_pair_stamped<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
-                               ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>>(
-        1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    // the product's pipelined kernel, built here with its stamps
+    return launch_pipe34<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
+                         ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>, QCN_PIPE34_D>(
+        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
     using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
@@ -195,6 +201,23 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
 // Copy kind's stamps of the last launch ([wg][t0, t1, r0, r1], n workgroups) to host.
 int qcn_clock_read(int kind, unsigned long long* host, int n) {
   if (kind < 0 || kind > 2 || n <= 0 || n > qcn::kClkMaxWg || !host) return QCN_ERR_ARG;
+  if (kind == 1 && g_last34_ws) {
+    // g_p34_stamp[wg] = [realtime start, memtime ..., realtime end]: the last
+    // nonzero entry is the end realtime, the one before it the end memtime
+    if (n > 1024) return QCN_ERR_ARG;
+    static unsigned long long st[1024][64];
+    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(qcn::g_p34_stamp), sizeof st, 0, hipMemcpyDeviceToHost) != hipSuccess)
+      return QCN_ERR_HIP;
+    for (int w = 0; w < n; ++w) {
+      int last = 63;
+      while (last > 3 && st[w][last] == 0) --last;
+      host[4 * w + 0] = st[w][1];
+      host[4 * w + 1] = st[w][last - 1];
+      host[4 * w + 2] = st[w][0];
+      host[4 * w + 3] = st[w][last];
+    }
+    return QCN_OK;
+  }
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_qcn_clk), (size_t)n * 32,
                              (size_t)kind * qcn::kClkMaxWg * 32, hipMemcpyDeviceToHost) == hipSuccess
              ? QCN_OK : QCN_ERR_HIP;

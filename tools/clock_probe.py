@@ -40,8 +40,8 @@ MFMA_MAC_PER_CLK_SIMD = 1024   # v_mfma_i32_32x32x32_i8: 32768 MAC per 32 cycles
 def grid_of(name, n, ncu):
     if name == "conv12":
         return min(n, ncu)
-    if name == "conv34":
-        return n                       # one 16x16 image (256 pixels) per 4-wave workgroup
+    if name == "conv34":               # persistent pipelined kernel above one image per CU,
+        return min(n, ncu) if n > ncu else n   # else one image per 8-wave workgroup
     if n <= ncu:                       # cout-split: two workgroups per pair of images
         return 2 * ((n + 1) // 2)
     return (n + 1) // 2                # two 8x8 images per 4-wave workgroup (convpair_ga_kernel)
