@@ -70,7 +70,9 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
-                  "conv34": ("convpair_kernel<qcn::ConvCfg<64, 128",),
+                  # (the persistent wave-specialised kernel above one image per CU,
+                  # the 8-wave one-image pair kernel at or below)
+                  "conv34": ("conv34ws_kernel", "convpair_kernel<qcn::ConvCfg<64, 128"),
                   # (one form runs per batch size: the split form at <= 1 image per CU)
                   "conv56": ("convpair_ga_kernel", "convpair_ga_split_kernel"),
                   # the two-launch head: "fc_finish" matches fc_finish_kernel (static)
