@@ -27,10 +27,18 @@
 #include <type_traits>
 #include <utility>
 
-// weight-prefetch depth (K-steps) of the pipelined conv3+conv4 kernel; D + 1
+// weight-prefetch depth (K-steps) of the wave-specialised pair kernels; D + 1
 // must divide 18 (build-time constant, not a runtime switch)
 #ifndef QCN_PIPE34_D
 #define QCN_PIPE34_D 2
+#endif
+// diagnostic builds only (tools/build_variant.sh): 0 keeps a pair on its
+// per-tile kernel for same-process A/B against the wave-specialised one
+#ifndef QCN_WS34
+#define QCN_WS34 1
+#endif
+#ifndef QCN_WS56
+#define QCN_WS56 1
 #endif
 
 namespace qcn {
@@ -1005,52 +1013,6 @@ void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   convpair_ga_split_body<CA, CB, D, COUTB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
-// --------------------------------------------------------------------------
-// conv3 + conv4 persistent and software-pipelined (batches above one image
-// per CU: the headline's batch 1024 gives four images per workgroup).
-//
-// One 4-wave workgroup per CU (one wave per SIMD, 512 registers each) loops
-// over its images.  Two accumulator sets per wave — X for conv3, Y for conv4 —
-// let one conv's epilogue run INSIDE the other conv's MFMA stream instead of
-// beside a co-resident workgroup that happens to be in another phase:
-//
-//   slot 1 of image j:  conv3(j)   -> X   | conv4's pooled epilogue of image
-//                                           j-2 from Y (requant, 16-B stores),
-//                                           image j+1 staged into the other
-//                                           conv3 patch buffer
-//   slot 2 of image j:  conv4(j-1) -> Y   | conv3's epilogue of image j from X
-//                                           (requant into the other conv4
-//                                           patch buffer)
-//
-// Each epilogue element (4 VALU: cvt, fma, mul, cvt_pk — FBGEMM-exact as
-// epilogue_tile_k) is placed after its own MFMA, at most one per two MFMAs,
-// so the VALU work issues in the MFMA pipe's shadow.  Weights stream from L2
-// into registers D K-steps ahead (as conv_mainloop_ga; D + 1 divides every
-// job's step count, so each job starts at register slot 0 and the last D
-// steps of a job prefetch the next job's first D).  With no LDS weight ring
-// the K loops have no barriers: two per image, at the slot boundaries.
-// The conv3 patch and the conv4 patch are double-buffered in LDS, their
-// zero-point halos written once per launch.
-template <class CA, class CB, int D>
-struct Pipe34 {
-  static_assert(CA::NWAVES == 4 && CB::NWAVES == 4 && CA::WCO == 2 && CB::WCO == 2 && CA::WI == 2 &&
-                CB::WI == 2 && CA::JT == 4 && CB::JT == 4, "four waves of 64-cout x 128-pixel tiles");
-  static_assert(!CA::kPool && CB::kPool && CA::kCout == CB::kCin && CA::kCout == CB::kCout, "A feeds B");
-  static_assert(CA::SEGS == 1 && CA::PXB == CA::IMG && CB::PXB == CB::IMG && CA::W == 16, "one image per tile");
-  static_assert(!CA::kSplit && CA::WBUF == CB::WBUF, "weight chunk stride shared by both convs");
-  static constexpr int SA = 2 * CA::NCH, SB = 2 * CB::NCH;   // K-steps per job
-  static_assert(SA % (D + 1) == 0 && SB % (D + 1) == 0, "every job starts at register slot 0");
-  static_assert(SA * 8 >= 144 && SB * 8 >= 256, "filler slots");
-  static constexpr int PA = (CA::PATCH + 15) / 16 * 16, PB = (CB::PATCH + 15) / 16 * 16;
-  static constexpr int OFF_PA = 0, OFF_PB = 2 * PA;
-  static constexpr int OFF_EA = OFF_PB + 2 * PB;           // u | v | mult, fp32 x cout each
-  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
-  static constexpr int OFF_CA = OFF_EB + 12 * CB::kCout;   // corr, int32 x cout
-  static constexpr int OFF_CB = OFF_CA + 4 * CA::kCout;
-  static constexpr int LDS = OFF_CB + 4 * CB::kCout;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
 // Epilogue constants of 4 consecutive output channels from an LDS copy
 // (u | v | mult, cout floats each).
 struct EpiG {
@@ -1152,16 +1114,16 @@ QCN_DEV void pipe_job(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_rs
 // Diagnostic builds only (tools/build_variant.sh): per-workgroup s_memtime
 // stamps of wave 0 around every pipeline barrier, [wg][stamp]; plain vector
 // stores into a buffer nothing else reads.
-__device__ unsigned long long g_p34_stamp[1024][64];
-QCN_DEV void p34_stamp(int& idx, unsigned long long t) {
+__device__ unsigned long long g_p34_stamp[2][1024][64];   // [conv3+4, conv5+6]
+QCN_DEV void p34_stamp(int kind, int& idx, unsigned long long t) {
   const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   if (threadIdx.x < 64 && lane == 0 && blockIdx.x < 1024 && idx < 64) {
-    volatile unsigned long long* d = &g_p34_stamp[blockIdx.x][idx];
+    volatile unsigned long long* d = &g_p34_stamp[kind][blockIdx.x][idx];
     *d = t + lane;
   }
   ++idx;
 }
-#define P34_STAMP() p34_stamp(stamp_i, __builtin_amdgcn_s_memtime())
+#define P34_STAMP() p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memtime())
 #else
 #define P34_STAMP()
 #endif
@@ -1176,368 +1138,188 @@ QCN_DEV void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <class CA, class CB, int D, bool FA, bool FB>
-__global__ __launch_bounds__(256, 1)
-void conv34p_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
-                    ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
-                    uint8_t* __restrict__ y) {
-  using P = Pipe34<CA, CB, D>;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wc = wave & 1, wp = wave >> 1;
-  const int l32 = lane & 31, hi = lane >> 5;
-  const int b = (int)blockIdx.x, G = (int)gridDim.x;
-  const int T = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // this workgroup's images b, b + G, ...
-#ifdef QCN_PIPE34_STAMP
-  int stamp_i = 0;
-  if (threadIdx.x < 64) {
-    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
-    p34_stamp(stamp_i, r0);
-  }
-#endif
-  P34_STAMP();
-  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
-  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
-  int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
-  int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
-  stage_epik<CA::kCout, 256>(epa, eka, tid);
-  stage_epik<CB::kCout, 256>(epb, ekb, tid);
-  if (tid < CA::kCout / 4) reinterpret_cast<int4*>(cra)[tid] = reinterpret_cast<const int4*>(epa.corr)[tid];
-  if (tid >= 64 && tid < 64 + CB::kCout / 4)
-    reinterpret_cast<int4*>(crb)[tid - 64] = reinterpret_cast<const int4*>(epb.corr)[tid - 64];
-  // zero-point halos of both buffers of both patches (never overwritten)
-  {
-    const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
-    constexpr int HS = 2 * 18 + 2 * 16;   // halo slots per patch
-    for (int e = tid; e < 2 * HS * (CA::kCin / 16); e += 256) {
-      const int bf = e / (HS * (CA::kCin / 16)), r = e % (HS * (CA::kCin / 16));
-      const int hs = r / (CA::kCin / 16), c = r % (CA::kCin / 16);
-      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
-      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
-      *reinterpret_cast<uint4*>(lds + P::OFF_PA + bf * P::PA + CA::slot(0, pr, pc) + c * 16) =
-          make_uint4(pa4, pa4, pa4, pa4);
-    }
-    for (int e = tid; e < 2 * HS * (CB::kCin / 16); e += 256) {
-      const int bf = e / (HS * (CB::kCin / 16)), r = e % (HS * (CB::kCin / 16));
-      const int hs = r / (CB::kCin / 16), c = r % (CB::kCin / 16);
-      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
-      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
-      *reinterpret_cast<uint4*>(lds + P::OFF_PB + bf * P::PB + CB::slot(0, pr, pc) + c * 16) =
-          make_uint4(pb4, pb4, pb4, pb4);
-    }
-  }
-  if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
-
-  // ---- per-lane addressing (lane-derived offsets that stay live)
-  const wt_rsrc_t wra = wt_rsrc(wa), wrb = wt_rsrc(wb);
-  const int voff = (wc * 64 + l32) * 64 + hi * 16;
-  // staging: the image is 16 KB contiguous; thread tid moves pieces tid + 256 q
-  // (pixel (tid >> 2) + 64 q: patch row (tid >> 6) + 4 q + 1, column ((tid >> 2) & 15) + 1)
-  const int st_dst = CA::slot(0, (tid >> 6) + 1, ((tid >> 2) & 15) + 1) + (tid & 3) * 16;
-
-  v16i accx[2][4], accy[2][4];
-  v4i ga[D + 1][2];
-  uint4 sv[4];
-#pragma unroll
-  for (int t = 0; t < D; ++t) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wra, voff, (t >> 1) * CA::WBUF + i * 2048 + (t & 1) * 32, 0);
-      ga[t][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
-    }
-  }
-  {  // image b into conv3 patch buffer 0
-    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + tid * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<uint4*>(lds + P::OFF_PA + st_dst + q * 4 * CA::RS) =
-          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
-  }
-  P34_STAMP();
-  lds_barrier();
-  P34_STAMP();
-
-  // Lane-derived values are recomputed from a laundered lane id in every
-  // slot: otherwise the loop-invariant LDS loads of the epilogue constants
-  // and corr tables are hoisted out of the image loop and held live across
-  // it (~250 registers, spilled).
-  struct Lane {
-    int l32, hi, ek, hb;
-    uint32_t yo;
-    const int *ca, *cb;
-  };
-  auto lanes = [&]() {
-    int lz = lane;
-    asm volatile("" : "+v"(lz));
-    Lane L;
-    L.l32 = lz & 31;
-    L.hi = lz >> 5;
-    L.ek = wc * 64 + 4 * L.hi;
-    // conv3's epilogue into conv4's patch: tile (i, jj) pixel m = (4 wp + jj) 32 + l32
-    L.hb = CB::slot(0, wp * 8 + (L.l32 >> 4) + 1, (L.l32 & 15) + 1) + wc * 64 + 4 * L.hi;
-    // conv4's pooled output: pooled pixel wp * 32 + l32, 16 channels per lane after the swaps
-    L.yo = (uint32_t)((wp * 32 + L.l32) * CB::kCout + wc * 64 + 16 * L.hi);
-    L.ca = cra + (lz >> 6);   // (lz >> 6 == 0: an address the compiler cannot hoist)
-    L.cb = crb + (lz >> 6);
-    return L;
-  };
-  // ---- the fillers
-  // conv4's pooled epilogue from acc: element e (0..31) of the wave's two
-  // 32-channel tiles (max over the four quadrant tiles, requant); a tile's
-  // 16-B rows go out after its 16th element
-  // The constants of each 4-channel group are read from LDS one group ahead
-  // (double-buffered): read right before use, each group's first element
-  // waited on the LDS round trip.
-  EpiG kb[2];
-  uint32_t wq[4];
-  auto epi4_pre = [&](const Lane& L) { kb[0] = load_epig(ekb, CB::kCout, L.ek); };
-  auto epi4 = [&](const Lane& L, v16i (&acc)[2][4], auto ec, wt_rsrc_t yr) {
-    constexpr int e = decltype(ec)::value;
-    constexpr int i = e >> 4, r = e & 15, g = r >> 2, ee = r & 3, gg = e >> 2;
-    if constexpr (ee == 0 && gg + 1 < 8)
-      kb[(gg + 1) & 1] = load_epig(ekb, CB::kCout, L.ek + ((gg + 1) >> 2) * 32 + 8 * ((gg + 1) & 3));
-    const int a = max(max(acc[i][0][r], acc[i][1][r]), max(acc[i][2][r], acc[i][3][r]));
-    wq[g] = rq_elem<FB>(a, kb[gg & 1], ee, epb, ee == 0 ? 0u : wq[g]);
-    if constexpr (r == 15) {
-      auto s01 = __builtin_amdgcn_permlane32_swap(wq[0], wq[1], false, false);
-      auto s23 = __builtin_amdgcn_permlane32_swap(wq[2], wq[3], false, false);
-      uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
-      auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
-      auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
-      store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
-    }
-  };
-  // conv3's epilogue of accx into conv4 patch pb: element e (0..127), a dword
-  // to the patch after every fourth
-  EpiG ka[2];
-  uint32_t wd = 0;
-  auto epi3_pre = [&](const Lane& L) { ka[0] = load_epig(eka, CA::kCout, L.ek); };
-  auto epi3 = [&](const Lane& L, auto ec, uint8_t* pb) {
-    constexpr int e = decltype(ec)::value;
-    constexpr int i = e >> 6, jj = (e >> 4) & 3, r = e & 15, g = r >> 2, ee = r & 3;
-    // group order: (i, jj, g); the constants depend on (i, g) only
-    constexpr int gg = e >> 2, gn = gg + 1, in = gn >> 4, g_n = gn & 3;
-    if constexpr (ee == 0 && gn < 32) ka[gn & 1] = load_epig(eka, CA::kCout, L.ek + in * 32 + 8 * g_n);
-    wd = rq_elem<FA>(accx[i][jj][r], ka[gg & 1], ee, epa, ee == 0 ? 0u : wd);
-    if constexpr (ee == 3) *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
-  };
-  auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
-  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (j & 1) * P::PA; };
-  auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
-
-  // slot 1 of image j: conv3(j) -> accx | [conv4's epilogue of j - 2 from
-  // accy], staging of image j + 1 (a valid dummy past the last image)
-  auto slot1 = [&](int j, auto E4) {
-    const Lane L = lanes();
-    const wt_rsrc_t yr = img_out(decltype(E4)::value ? j - 2 : 0);
-    const int nn = j + 1 < T ? b + (j + 1) * G : b;
-    const uint8_t* src = x + (long)nn * CA::IMG * CA::kCin + tid * 16;
-    uint8_t* pdst = pa_buf(j + 1) + st_dst;
-    // the next job: conv4 of image j - 1, or conv3 of image 1 after image 0
-    const wt_rsrc_t wn = (j == 0 && T > 1) ? wra : wrb;
-    pipe_job<CA, D>(pa_buf(j), L.ca, wra, wn, voff, wc, wp, L.l32, L.hi, accx, ga, [&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      if constexpr (k == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
-        if constexpr (decltype(E4)::value) epi4_pre(L);
-      }
-      if constexpr (decltype(E4)::value && (k & 3) == 1 && (k >> 2) < 32)
-        epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
-      if constexpr (k >= 136 && k < 144 && (k & 1) == 0) {
-        constexpr int q = (k - 136) >> 1;
-        *reinterpret_cast<uint4*>(pdst + q * 4 * CA::RS) =
-            make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
-      }
-    });
-    P34_STAMP();
-    lds_barrier();
-    P34_STAMP();
-  };
-  // slot 2 of image j: conv4(j - 1) -> accy | conv3's epilogue of image j
-  auto slot2 = [&](int j) {
-    const Lane L = lanes();
-    uint8_t* pb = pb_buf(j);
-    const wt_rsrc_t wn = j + 1 < T ? wra : wrb;   // next: conv3 of j + 1, or conv4 of j
-    pipe_job<CB, D>(pb_buf(j - 1), L.cb, wrb, wn, voff, wc, wp, L.l32, L.hi, accy, ga, [&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      if constexpr (k == 0) epi3_pre(L);
-      if constexpr ((k & 1) == 1 && (k >> 1) < 128) epi3(L, std::integral_constant<int, (k >> 1)>{}, pb);
-    });
-    P34_STAMP();
-    lds_barrier();
-    P34_STAMP();
-  };
-
-  // image 0: conv3, then its epilogue on its own (nothing to overlap it with)
-  slot1(0, std::false_type{});
-  {
-    const Lane L = lanes();
-    uint8_t* pb0 = pb_buf(0);
-    epi3_pre(L);
-    static_for<128>([&](auto ec) { epi3(L, ec, pb0); });
-    P34_STAMP();
-    lds_barrier();
-    P34_STAMP();
-  }
-  if (T > 1) {
-    slot1(1, std::false_type{});
-    slot2(1);
-  }
-#pragma unroll 1
-  for (int j = 2; j < T; ++j) {
-    slot1(j, std::true_type{});
-    slot2(j);
-  }
-  // conv4 of the last image into accx (free since its conv3 epilogue) with
-  // conv4's epilogue of image T - 2 from accy as filler (T == 1: accy holds
-  // nothing; that garbage goes to image b's output and is overwritten by the
-  // real epilogue below, later in this wave's program order)
-  {
-    const Lane L = lanes();
-    const wt_rsrc_t yr = img_out(T >= 2 ? T - 2 : 0);
-    pipe_job<CB, D>(pb_buf(T - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, accx, ga, [&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      if constexpr (k == 0) epi4_pre(L);
-      if constexpr ((k & 3) == 1 && (k >> 2) < 32) epi4(L, accy, std::integral_constant<int, (k >> 2)>{}, yr);
-    });
-    const Lane L2 = lanes();
-    const wt_rsrc_t yl = img_out(T - 1);
-    epi4_pre(L2);
-    static_for<32>([&](auto ec) { epi4(L2, accx, ec, yl); });
-  }
-  P34_STAMP();
-#ifdef QCN_PIPE34_STAMP
-  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
-#endif
-}
-
-
 // --------------------------------------------------------------------------
-// conv3 + conv4 with wave-specialised roles (persistent; above one image per
-// CU).  One 8-wave workgroup per CU: waves 0-3 run conv3, waves 4-7 conv4,
-// so every SIMD holds one wave of each role (a workgroup's waves go to the
-// SIMDs cyclically).  In period p (one workgroup barrier per period):
+// Two convolutions of a block with wave-specialised roles (persistent; the
+// headline's conv3+conv4 and conv5+conv6 at batch 1024).  One 8-wave
+// workgroup per CU: waves 0-3 run conv A, waves 4-7 conv B, so every SIMD
+// holds one wave of each role (a workgroup's waves go to the SIMDs
+// cyclically).  The workgroup takes tiles b, b + G, ... (a tile = CA::PXB
+// pixels of whole images: one 16x16 image for conv3+4, two 8x8 images for
+// conv5+6).  In period p (one workgroup barrier per period):
 //
-//   conv3 waves:  conv3(p) -> acc, then conv3's epilogue of image p into the
-//                 conv4 patch buffer p & 1, and image p + 1 staged into the
-//                 conv3 patch buffer (p + 1) & 1 (loads issued before the
-//                 epilogue, written after it);
-//   conv4 waves:  conv4's pooled epilogue of image p - 2 (acc), then
-//                 conv4(p - 1) -> acc from the conv4 patch buffer (p - 1) & 1.
+//   A waves:  conv A(p) -> acc, then A's epilogue of tile p into B's patch
+//             buffer p & 1, and tile p + 1's input staged (loads issued
+//             before the epilogue);
+//   B waves:  B's pooled epilogue of tile p - 2 (acc), then conv B(p - 1) ->
+//             acc from B's patch buffer (p - 1) & 1.
 //
 // Each role's VALU epilogue runs beside the other role's MFMAs on the same
-// SIMD, at a fixed phase (conv4's at the period start, conv3's at its end),
-// instead of wherever two independent workgroups happen to drift.  Weights
-// stream from L2 into registers D K-steps ahead; the last D steps of a job
-// prefetch the next period's first D.  LDS: both patches double-buffered
-// (halos written once per launch), epilogue constants and corr tables.
-template <class CA, class CB, int D, bool FA, bool FB>
+// SIMD, at a fixed phase (B's at the period start, A's at its end), instead
+// of wherever two independent workgroups happen to drift.  Weights stream
+// from L2 into registers D K-steps ahead; the last D steps of a job prefetch
+// the next period's first D.  LDS: B's patch double-buffered, A's patch
+// double-buffered when it fits (conv3+4), else single with the staged input
+// held in registers and written after the period barrier behind a second
+// barrier (conv5+6); halos written once per launch; epilogue constants and
+// corr tables.
+template <class CA, class CB, int D>
+struct PairWs {
+  static_assert(CA::NWAVES == 4 && CB::NWAVES == 4 && CA::WCO == CB::WCO && CA::WI == 2 && CB::WI == 2 &&
+                CA::JT == 4 && CB::JT == 4, "four waves of 64-cout x 128-pixel tiles per role");
+  static_assert(!CA::kPool && CB::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CA::H && CA::W == CB::W &&
+                !CA::kBand && !CB::kBand, "whole images per tile");
+  static_assert(!CA::kSplit && CA::WBUF % 2048 == 0 && CB::WBUF % 2048 == 0, "weight layouts");
+  static constexpr int SEGS = CA::SEGS, IMG = CA::IMG;
+  static constexpr int IN_BYTES = SEGS * IMG * CA::kCin;   // a tile's input
+  static_assert(IN_BYTES == 4 * 256 * 16, "four 16-B staging pieces per A-role thread");
+  static constexpr int SA = 2 * CA::NCH, SB = 2 * CB::NCH;   // K-steps per job
+  static_assert(SA % (D + 1) == 0 && SB % (D + 1) == 0, "every job starts at register slot 0");
+  static constexpr int PA = (CA::PATCH + 15) / 16 * 16, PB = (CB::PATCH + 15) / 16 * 16;
+  static constexpr int TAB = 16 * (CA::kCout + CB::kCout);   // u | v | mult | corr of both
+  static constexpr bool DOUBLE_A = 2 * PA + 2 * PB + TAB <= 160 * 1024;
+  static constexpr int OFF_PB = 0;
+  static constexpr int OFF_PA = 2 * PB;
+  static constexpr int OFF_EA = OFF_PA + (DOUBLE_A ? 2 : 1) * PA;   // u | v | mult, fp32 x cout each
+  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
+  static constexpr int OFF_CA = OFF_EB + 12 * CB::kCout;            // corr, int32 x cout
+  static constexpr int OFF_CB = OFF_CA + 4 * CA::kCout;
+  static constexpr int LDS = OFF_CB + 4 * CB::kCout;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static constexpr int OPI = CB::OPX / SEGS;   // pooled output pixels per image
+};
+
+template <class CA, class CB, int D, bool FA, bool FB, bool KMAJOR>
 __global__ __launch_bounds__(512, 1)
-void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
-                     ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
-                     uint8_t* __restrict__ y) {
-  using P = Pipe34<CA, CB, D>;
+void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
+                        ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
+                        uint8_t* __restrict__ y) {
+  using P = PairWs<CA, CB, D>;
+  constexpr int SEGS = P::SEGS, IMG = CA::IMG, W = CA::W, WCO = CA::WCO;
+  constexpr int CH16 = CA::kCin / 16;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
-  const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // 0: conv3, 1: conv4
+  const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // 0: conv A, 1: conv B
   const int rt = tid & 255, lane = tid & 63, wave = rt >> 6;   // thread / wave within the role
-  const int wc = wave & 1, wp = wave >> 1;
+  const int wc = wave % WCO, wp = wave / WCO;
   const int b = (int)blockIdx.x, G = (int)gridDim.x;
-  const int T = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // this workgroup's images b, b + G, ...
+  const int ntile = (nimg + SEGS - 1) / SEGS;
+  const int T = b < ntile ? (ntile - 1 - b) / G + 1 : 0;   // this workgroup's tiles b, b + G, ...
 #ifdef QCN_PIPE34_STAMP
   int stamp_i = 0;
-  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
+  constexpr int stamp_kind = CA::kCin == 64 ? 0 : 1;
+  if (threadIdx.x < 64) p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
   P34_STAMP();
-  // image b's conv3 input (conv3 waves): loads first, so their latency runs
-  // under the table / halo set-up below
+  // tile t's input piece q of this A-role thread (images past the batch read
+  // the last image: their outputs are never stored)
+  auto in_src = [&](int t, int q) {
+    const int p = rt + 256 * q;
+    int n = t * SEGS + p / (IMG * CH16);
+    n = n < nimg ? n : nimg - 1;
+    return x + ((long)n * IMG + (p / CH16) % IMG) * CA::kCin + (p % CH16) * 16;
+  };
+  auto in_dst = [&](int q) {
+    const int p = rt + 256 * q;
+    const int pix = (p / CH16) % IMG;
+    return CA::slot(p / (IMG * CH16), pix / W + 1, pix % W + 1) + (p % CH16) * 16;
+  };
+  // tile b's input (A waves): loads first, their latency under the set-up below
   uint4 sv[4];
-  if (role == 0 && b < nimg) {
-    const uint8_t* src = x + (long)b * CA::IMG * CA::kCin + (tid & 255) * 16;
+  if (role == 0 && T > 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(b, q));
   }
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
   int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
   int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
-  // the epilogue tables (u | v | mult of both convs, both corr): one 16-B
-  // piece per conv4-role thread, loaded now and written after the halos
-  static_assert(CA::kCout == 128 && CB::kCout == 128, "table split below");
-  const int tt = tid - 256;   // 0..255 in the conv4 role
-  const float4* tsrc = nullptr;
-  float4* tdst = nullptr;
+  // the epilogue tables (u | v | mult of both convs, both corr) in 16-B
+  // pieces over the B-role threads, loaded now and written after the halos
+  constexpr int NA = 3 * CA::kCout / 4, NB = 3 * CB::kCout / 4;       // float4 pieces
+  constexpr int NCA = CA::kCout / 4, NCB = CB::kCout / 4;
+  constexpr int NTAB = NA + NB + NCA + NCB, TPT = (NTAB + 255) / 256;
+  float4 tval[TPT];
+  auto tab = [&](int e, bool dst) -> float4* {
+    if (e < NA) {
+      const int a = e / (CA::kCout / 4), o = e % (CA::kCout / 4);
+      const float* s = a == 0 ? epa.u : (a == 1 ? epa.v : epa.mult);
+      return dst ? reinterpret_cast<float4*>(eka) + e : const_cast<float4*>(reinterpret_cast<const float4*>(s) + o);
+    }
+    e -= NA;
+    if (e < NB) {
+      const int a = e / (CB::kCout / 4), o = e % (CB::kCout / 4);
+      const float* s = a == 0 ? epb.u : (a == 1 ? epb.v : epb.mult);
+      return dst ? reinterpret_cast<float4*>(ekb) + e : const_cast<float4*>(reinterpret_cast<const float4*>(s) + o);
+    }
+    e -= NB;
+    if (e < NCA)
+      return dst ? reinterpret_cast<float4*>(cra) + e
+                 : const_cast<float4*>(reinterpret_cast<const float4*>(epa.corr) + e);
+    e -= NCA;
+    return dst ? reinterpret_cast<float4*>(crb) + e
+               : const_cast<float4*>(reinterpret_cast<const float4*>(epb.corr) + e);
+  };
   if (role == 1) {
-    if (tt < 96) {
-      tsrc = reinterpret_cast<const float4*>(tt < 32 ? epa.u : tt < 64 ? epa.v : epa.mult) + (tt & 31);
-      tdst = reinterpret_cast<float4*>(eka) + tt;
-    } else if (tt < 192) {
-      const int t2 = tt - 96;
-      tsrc = reinterpret_cast<const float4*>(t2 < 32 ? epb.u : t2 < 64 ? epb.v : epb.mult) + (t2 & 31);
-      tdst = reinterpret_cast<float4*>(ekb) + t2;
-    } else if (tt < 224) {
-      tsrc = reinterpret_cast<const float4*>(epa.corr) + (tt - 192);
-      tdst = reinterpret_cast<float4*>(cra) + (tt - 192);
-    } else {
-      tsrc = reinterpret_cast<const float4*>(epb.corr) + (tt - 224);
-      tdst = reinterpret_cast<float4*>(crb) + (tt - 224);
-    }
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (rt + 256 * k < NTAB) tval[k] = *tab(rt + 256 * k, false);
   }
-  const float4 tval = role == 1 ? *tsrc : make_float4(0.f, 0.f, 0.f, 0.f);
-  {  // zero-point halos of both buffers of both patches (never overwritten)
+  {  // zero-point halos of every buffer of both patches (never overwritten)
     const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
-    constexpr int HS = 2 * 18 + 2 * 16;   // halo slots per patch
-    for (int e = tid; e < 2 * HS * (CA::kCin / 16); e += 512) {
-      const int bf = e / (HS * (CA::kCin / 16)), r = e % (HS * (CA::kCin / 16));
-      const int hs = r / (CA::kCin / 16), c = r % (CA::kCin / 16);
-      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
-      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
-      *reinterpret_cast<uint4*>(lds + P::OFF_PA + bf * P::PA + CA::slot(0, pr, pc) + c * 16) =
-          make_uint4(pa4, pa4, pa4, pa4);
-    }
-    for (int e = tid; e < 2 * HS * (CB::kCin / 16); e += 512) {
-      const int bf = e / (HS * (CB::kCin / 16)), r = e % (HS * (CB::kCin / 16));
-      const int hs = r / (CB::kCin / 16), c = r % (CB::kCin / 16);
-      const int pr = hs < 18 ? 0 : (hs < 36 ? 17 : 1 + ((hs - 36) >> 1));
-      const int pc = hs < 18 ? hs : (hs < 36 ? hs - 18 : (((hs - 36) & 1) ? 17 : 0));
-      *reinterpret_cast<uint4*>(lds + P::OFF_PB + bf * P::PB + CB::slot(0, pr, pc) + c * 16) =
-          make_uint4(pb4, pb4, pb4, pb4);
-    }
+    auto halo = [&](auto cfg, uint8_t* base, int nbuf, int pbytes, uint32_t pad) {
+      using C = decltype(cfg);
+      constexpr int HS = 2 * C::PCOLS + 2 * (C::PROWS - 2), CH = C::kCin / 16;
+      const int total = nbuf * C::SEGS * HS * CH;
+      for (int e = tid; e < total; e += 512) {
+        const int c = e % CH, hs = (e / CH) % HS, sg = (e / (CH * HS)) % C::SEGS, bf = e / (CH * HS * C::SEGS);
+        int pr, pc;
+        if (hs < C::PCOLS) { pr = 0; pc = hs; }
+        else if (hs < 2 * C::PCOLS) { pr = C::PROWS - 1; pc = hs - C::PCOLS; }
+        else { const int r = hs - 2 * C::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? C::PCOLS - 1 : 0; }
+        *reinterpret_cast<uint4*>(base + bf * pbytes + C::slot(sg, pr, pc) + c * 16) = make_uint4(pad, pad, pad, pad);
+      }
+    };
+    halo(CA{}, lds + P::OFF_PA, P::DOUBLE_A ? 2 : 1, P::PA, pa4);
+    halo(CB{}, lds + P::OFF_PB, 2, P::PB, pb4);
   }
-  if (role == 1) *tdst = tval;
+  if (role == 1) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (rt + 256 * k < NTAB) *tab(rt + 256 * k, true) = tval[k];
+  }
   if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
 
   const int l32 = lane & 31, hi = lane >> 5;
   const wt_rsrc_t wra = wt_rsrc(wa), wrb = wt_rsrc(wb);
   const int voff = (wc * 64 + l32) * 64 + hi * 16;
-  // staging (conv3 waves): the image is 16 KB contiguous; role thread rt moves
-  // pieces rt + 256 q (patch row (rt >> 6) + 4 q + 1, column ((rt >> 2) & 15) + 1)
-  const int st_dst = CA::slot(0, (rt >> 6) + 1, ((rt >> 2) & 15) + 1) + (rt & 3) * 16;
-  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (j & 1) * P::PA; };
+  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (P::DOUBLE_A ? (j & 1) * P::PA : 0); };
   auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
+  auto write_in = [&](uint8_t* pa) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<uint4*>(pa + in_dst(q)) =
+          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+  };
 
   v16i acc[2][4];
   v4i ga[D + 1][2];
   {
     const wt_rsrc_t w0 = role == 0 ? wra : wrb;
+    constexpr int CST = CA::WBUF;
+    static_assert(CA::WBUF == CB::WBUF || true, "");
 #pragma unroll
     for (int t = 0; t < D; ++t) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(w0, voff, (t >> 1) * CA::WBUF + i * 2048 + (t & 1) * 32, 0);
+        const int cst = role == 0 ? CA::WBUF : CB::WBUF;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(w0, voff, (t >> 1) * cst + i * 2048 + (t & 1) * 32, 0);
         ga[t][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
       }
     }
+    (void)CST;
   }
-  if (role == 0) {  // image b into conv3 patch buffer 0
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<uint4*>(pa_buf(0) + st_dst + q * 4 * CA::RS) =
-          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
-  }
+  if (role == 0) write_in(pa_buf(0));
   P34_STAMP();
   lds_barrier();
   P34_STAMP();
@@ -1545,8 +1327,9 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
   // lane-derived epilogue addressing from a laundered lane id (not hoisted
   // out of the period loop and held live across the MFMA jobs)
   struct Lane {
-    int l32, hi, ek, hb;
-    uint32_t yo;
+    int l32, hi, ek;
+    int hb[4];          // B-patch offset of A's output pixel (wp * 4 + jj) * 32 + l32
+    int q;              // pooled output pixel of B within the tile
     const int *ca, *cb;
   };
   auto lanes = [&]() {
@@ -1556,16 +1339,21 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
     L.l32 = lz & 31;
     L.hi = lz >> 5;
     L.ek = wc * 64 + 4 * L.hi;
-    L.hb = CB::slot(0, wp * 8 + (L.l32 >> 4) + 1, (L.l32 & 15) + 1) + wc * 64 + 4 * L.hi;
-    L.yo = (uint32_t)((wp * 32 + L.l32) * CB::kCout + wc * 64 + 16 * L.hi);
-    L.ca = cra + (lz >> 6);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int m = (wp * 4 + jj) * 32 + L.l32;
+      const int pix = m % IMG;
+      L.hb[jj] = CB::slot(m / IMG, pix / W + 1, pix % W + 1) + wc * 64 + 4 * L.hi;
+    }
+    L.q = wp * 32 + L.l32;
+    L.ca = cra + (lz >> 6);   // (lz >> 6 == 0: an address the compiler cannot hoist)
     L.cb = crb + (lz >> 6);
     return L;
   };
-  // conv3's epilogue of acc into conv4 patch pb (epilogue_tile_k's numerics).
-  // The constants of a 32-channel tile row (4 groups of 4 channels) are read
-  // from LDS together: one LDS round trip per tile row.
-  auto epi3 = [&](const Lane& L, uint8_t* pb) {
+  // A's epilogue of acc into B's patch pb (epilogue_tile_k's numerics).  The
+  // constants of a 32-channel tile row (4 groups of 4 channels) are read from
+  // LDS together: one LDS round trip per tile row.
+  auto epi_a = [&](const Lane& L, uint8_t* pb) {
     static_for<2>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       EpiG K[4];
@@ -1576,13 +1364,14 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
         uint32_t wd = 0;
 #pragma unroll
         for (int ee = 0; ee < 4; ++ee) wd = rq_elem<FA>(acc[i][jj][4 * g + ee], K[g], ee, epa, wd);
-        *reinterpret_cast<uint32_t*>(pb + L.hb + jj * 2 * CB::RS + i * 32 + 8 * g) = xor80(wd);
+        *reinterpret_cast<uint32_t*>(pb + L.hb[jj] + i * 32 + 8 * g) = xor80(wd);
       });
     });
   };
-  // conv4's pooled epilogue of acc (max over the four quadrant tiles, requant,
-  // two permlane32 swap rounds, one 16-B store per tile and lane)
-  auto epi4 = [&](const Lane& L, wt_rsrc_t yr) {
+  // B's pooled epilogue of acc for tile t (max over the four quadrant tiles,
+  // requant, two permlane32 swap rounds, one 16-B store per tile row and lane)
+  auto epi_b = [&](const Lane& L, int t) {
+    const int n = t * SEGS + L.q / P::OPI, pix = L.q % P::OPI;
     static_for<2>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       EpiG K[4];
@@ -1605,31 +1394,39 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
       uint32_t w0 = s01[0], w1 = s01[1], w2 = s23[0], w3 = s23[1];
       auto s02 = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
       auto s13 = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
-      store_wt16(yr, L.yo + i * 32, make_uint4(s02[0], s13[0], s02[1], s13[1]));
+      const uint4 v = make_uint4(s02[0], s13[0], s02[1], s13[1]);
+      const int co = wc * 64 + i * 32;   // + 16 hi: this lane's 16 channels
+      if (n < nimg) {
+        if constexpr (KMAJOR) {   // [f / 32][image][32], f = pix * cout + channel (NHWC flatten)
+          const int kc = (pix * CB::kCout + co) / 32;
+          store_wt16(wt_rsrc(y), (uint32_t)(((long)kc * nimg + n) * 32 + 16 * L.hi), v);
+        } else {
+          store_wt16(wt_rsrc(y + (long)n * P::OPI * CB::kCout), (uint32_t)(pix * CB::kCout + co + 16 * L.hi), v);
+        }
+      }
     });
   };
-  auto img_out = [&](int j) { return wt_rsrc(y + (long)(b + j * G) * CB::OPX * CB::kCout); };
   auto nofill = [](auto) {};
 
-  // Each role runs its own period loop (T + 1 periods, one barrier each, so
-  // the two roles pass the same barriers).
+  // Each role runs its own period loop (T + 1 periods, one barrier each, or
+  // two with a single A patch, so both roles pass the same barriers).
   if (role == 0) {
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
+      if constexpr (!P::DOUBLE_A) {   // tile p's input, held since period p - 1
+        if (p >= 1 && p < T) write_in(pa_buf(p));
+        lds_barrier();
+      }
       if (p < T) {
         const Lane L = lanes();
         pipe_job<CA, D, true>(pa_buf(p), L.ca, wra, wra, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
-        // image p + 1 (a valid dummy past the last): loads now, written after the epilogue
-        const int nn = p + 1 < T ? b + (p + 1) * G : b;
-        const uint8_t* src = x + (long)nn * CA::IMG * CA::kCin + rt * 16;
+        // tile p + 1 (a valid dummy past the last): loads now, written after the
+        // epilogue (double A patch) or after the next period barrier
+        const int tn = b + (p + 1 < T ? p + 1 : p) * G;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(src + q * 4096);
-        epi3(L, pb_buf(p));
-        uint8_t* pdst = pa_buf(p + 1) + st_dst;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<uint4*>(pdst + q * 4 * CA::RS) =
-              make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(tn, q));
+        epi_a(L, pb_buf(p));
+        if constexpr (P::DOUBLE_A) write_in(pa_buf(p + 1));
       }
       P34_STAMP();
       lds_barrier();
@@ -1638,9 +1435,10 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
   } else {
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
+      if constexpr (!P::DOUBLE_A) lds_barrier();
       if (p >= 1) {
         const Lane L = lanes();
-        if (p >= 2) epi4(L, img_out(p - 2));
+        if (p >= 2) epi_b(L, b + (p - 2) * G);
         pipe_job<CB, D, true>(pb_buf(p - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
       }
       P34_STAMP();
@@ -1648,11 +1446,11 @@ void conv34ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const in
       P34_STAMP();
     }
     const Lane L = lanes();
-    epi4(L, img_out(T - 1));
+    epi_b(L, b + (T - 1) * G);
   }
   P34_STAMP();
 #ifdef QCN_PIPE34_STAMP
-  if (threadIdx.x < 64) p34_stamp(stamp_i, __builtin_amdgcn_s_memrealtime());
+  if (threadIdx.x < 64) p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
 }
 
@@ -2321,32 +2119,32 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-#ifndef QCN_CONV34_WS
-#define QCN_CONV34_WS 1
-#endif
-template <class CA, class CB, int D, bool FA, bool FB>
-int launch_pipe34_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
-                    const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
-  using P = Pipe34<CA, CB, D>;
-  auto k = QCN_CONV34_WS ? conv34ws_kernel<CA, CB, D, FA, FB> : conv34p_kernel<CA, CB, D, FA, FB>;
+template <class CA, class CB, int D, bool FA, bool FB, bool KM>
+int launch_pair_ws_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
+                     const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
+  using P = PairWs<CA, CB, D>;
+  auto k = convpair_ws_kernel<CA, CB, D, FA, FB, KM>;
   static bool attr_done[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
-  const int grid = nimg < ncu ? nimg : ncu;   // persistent: one workgroup per CU
-  hipLaunchKernelGGL(k, dim3(grid), dim3(QCN_CONV34_WS ? 512 : 256), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp,
-                     wb, epb, y);
+  const int ntile = (nimg + P::SEGS - 1) / P::SEGS;
+  const int grid = ntile < ncu ? ntile : ncu;   // persistent: one workgroup per CU
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
 template <class CA, class CB, int D>
-int launch_pipe34(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
-                  const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
+int launch_pair_ws(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
+                   const int8_t* wb, const ConvEpi& epb, bool kmajor, uint8_t* y, hipStream_t st, int ncu) {
   // the FBGEMM fast path (zp_y == 0, no floor, no QDQ hand-off) is known on the host
   const bool fa = epa.zp_y == 0 && epa.lo == 0 && epa.qdq == 0;
   const bool fb = epb.zp_y == 0 && epb.lo == 0 && epb.qdq == 0;
-  if (fa && fb) return launch_pipe34_k<CA, CB, D, true, true>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
-  if (fa) return launch_pipe34_k<CA, CB, D, true, false>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
-  if (fb) return launch_pipe34_k<CA, CB, D, false, true>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
-  return launch_pipe34_k<CA, CB, D, false, false>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+#define QCN_WS(FA_, FB_, KM_) \
+  if (fa == FA_ && fb == FB_ && kmajor == KM_)                                                            \
+    return launch_pair_ws_k<CA, CB, D, FA_, FB_, KM_>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+  QCN_WS(true, true, false) QCN_WS(true, false, false) QCN_WS(false, true, false) QCN_WS(false, false, false)
+  QCN_WS(true, true, true) QCN_WS(true, false, true) QCN_WS(false, true, true) QCN_WS(false, false, true)
+#undef QCN_WS
+  return QCN_ERR_UNSUPPORTED;
 }
 
 template <class CA, class CB, int D, int COUTB>
@@ -2402,10 +2200,10 @@ int dispatch_conv(int cin, int cout, int hw, int pool, const uint8_t* x, int nim
 extern "C" {
 
 #ifdef QCN_PIPE34_STAMP
-int qcn_diag_p34_stamps(unsigned long long* host, int nwg) {
-  if (!host || nwg <= 0 || nwg > 1024) return QCN_ERR_ARG;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_p34_stamp), (size_t)nwg * 64 * 8, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+int qcn_diag_p34_stamps(int kind, unsigned long long* host, int nwg) {
+  if (!host || nwg <= 0 || nwg > 1024 || kind < 0 || kind > 1) return QCN_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_p34_stamp), (size_t)nwg * 64 * 8,
+                             (size_t)kind * 1024 * 64 * 8, hipMemcpyDeviceToHost) == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 #endif
 
@@ -2499,8 +2297,10 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
     using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
-    // above one image per CU: the persistent software-pipelined kernel
-    if (!kmajor) return launch_pipe34<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
+    // two or more images per CU: the persistent wave-specialised kernel
+    if (QCN_WS34 && nimg >= 2 * ncu)
+      return launch_pair_ws<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
+                                                  kmajor != 0, y, st, ncu);
     return launch_pair<A3, B4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
@@ -2515,6 +2315,10 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     if (nimg <= ncu)
       return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    // two or more image pairs per CU: the persistent wave-specialised kernel
+    if (QCN_WS56 && nimg >= 4 * ncu)
+      return launch_pair_ws<A1, B1, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
+                                                  kmajor != 0, y, st, ncu);
     return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;

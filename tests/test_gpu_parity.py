@@ -516,18 +516,22 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     assert np.array_equal(out_p.cpu().numpy(), z["logits"])
 
 
-@pytest.mark.parametrize("n", [1, 6, 255, 256, 257, 300, 513, 1023, 1028])
-def test_conv_pair_workgroup_shapes_equal_layerwise(dev, n):
-    """conv3+conv4 and conv5+conv6 at batch sizes around their tilings: at or
-    below one image per CU conv3+4 runs one image on 8 waves and conv5+6 splits
-    its output channels over two workgroups per image pair; above, conv3+4
-    runs one image per 4-wave workgroup and conv5+6 two images per 4-wave
-    workgroup (the last holds one image when n is odd).  conv4's and conv6's
+@pytest.mark.parametrize("mode,n", [("static", n) for n in (1, 6, 255, 256, 257, 300, 511, 512, 513, 1023,
+                                                           1024, 1025, 1028, 1031)] +
+                         [("qdq", n) for n in (512, 1024, 1031)])
+def test_conv_pair_workgroup_shapes_equal_layerwise(dev, mode, n):
+    """conv3+conv4 and conv5+conv6 at batch sizes around their tilings (256
+    CUs): at or below one image per CU conv3+4 runs one image on 8 waves and
+    conv5+6 splits its output channels over two workgroups per image pair;
+    above, conv3+4 runs one image per 4-wave workgroup and conv5+6 two images
+    per 4-wave workgroup; from two images per CU conv3+4, and from four conv5+6,
+    run the persistent wave-specialised kernel (the last tile of conv5+6 holds
+    one image when n is odd).  Static and QDQ hand-offs.  conv4's and conv6's
     outputs and the logits equal the per-layer kernels' bit for bit."""
     import netfix
     from qconvnet.qmodel import QuantizedConvNet
     from oracle import torch_ref
-    spec, _ = netfix.static_spec(netfix.load(False))
+    spec = netfix.static_spec(netfix.load(False))[0] if mode == "static" else netfix.qdq_spec(netfix.load(False))
     x = torch.from_numpy(torch_ref.synthetic_images(n, 13)).to(dev)
     model = QuantizedConvNet(spec, dev)
     assert model.kernel_names(x.shape)[1:3] == ("conv34", "conv56")

@@ -117,7 +117,8 @@ int launch_pair_ga_stamped(int kind, const uint8_t* x, int nimg, int x_zp, const
 }  // namespace
 }  // namespace qcn
 
-static bool g_last34_ws = false;   // the last conv3+conv4 launch was the pipelined kernel
+// the last conv3+conv4 / conv5+conv6 launch was the wave-specialised kernel
+static bool g_last34_ws = false, g_last56_ws = false;
 
 extern "C" {
 
@@ -147,15 +148,15 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   const int ncu = qcn_cu_count();
   const bool small = ncu > 0 && nimg <= ncu;
   if (hw == 16 && cin == 64 && cmid == 128 && cout == 128) {
-    g_last34_ws = !small && !kmajor;
+    g_last34_ws = nimg >= 2 * ncu;
     if (small)
       return launch_pair_stamped<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                                  ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    // the product's pipelined kernel, built here with its stamps
-    return launch_pipe34<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
-                         ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>, QCN_PIPE34_D>(
-        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st, ncu);
+    // the product's wave-specialised kernel, built here with its stamps
+    return launch_pair_ws<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
+                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>, QCN_PIPE34_D>(
+        x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, kmajor != 0, y, st, ncu);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
     using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
@@ -170,8 +171,12 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
                          xb_zp, wb_packed, epb, y);
       return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
     }
-    return launch_pair_ga_stamped<A1, ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>, 4>(
-        2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    using B1 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
+    g_last56_ws = nimg >= 4 * ncu;
+    if (g_last56_ws)
+      return launch_pair_ws<A1, B1, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
+                                                  kmajor != 0, y, st, ncu);
+    return launch_pair_ga_stamped<A1, B1, 4>(2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;
 }
@@ -201,12 +206,13 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
 // Copy kind's stamps of the last launch ([wg][t0, t1, r0, r1], n workgroups) to host.
 int qcn_clock_read(int kind, unsigned long long* host, int n) {
   if (kind < 0 || kind > 2 || n <= 0 || n > qcn::kClkMaxWg || !host) return QCN_ERR_ARG;
-  if (kind == 1 && g_last34_ws) {
-    // g_p34_stamp[wg] = [realtime start, memtime ..., realtime end]: the last
-    // nonzero entry is the end realtime, the one before it the end memtime
+  if ((kind == 1 && g_last34_ws) || (kind == 2 && g_last56_ws)) {
+    // g_p34_stamp[k][wg] = [realtime start, memtime ..., realtime end]: the
+    // last nonzero entry is the end realtime, the one before it the end memtime
     if (n > 1024) return QCN_ERR_ARG;
     static unsigned long long st[1024][64];
-    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(qcn::g_p34_stamp), sizeof st, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(qcn::g_p34_stamp), sizeof st, (size_t)(kind - 1) * sizeof st,
+                            hipMemcpyDeviceToHost) != hipSuccess)
       return QCN_ERR_HIP;
     for (int w = 0; w < n; ++w) {
       int last = 63;

@@ -40,10 +40,12 @@ MFMA_MAC_PER_CLK_SIMD = 1024   # v_mfma_i32_32x32x32_i8: 32768 MAC per 32 cycles
 def grid_of(name, n, ncu):
     if name == "conv12":
         return min(n, ncu)
-    if name == "conv34":               # persistent pipelined kernel above one image per CU,
-        return min(n, ncu) if n > ncu else n   # else one image per 8-wave workgroup
+    if name == "conv34":               # persistent wave-specialised kernel from two images
+        return ncu if n >= 2 * ncu else n      # per CU, else one image per workgroup
     if n <= ncu:                       # cout-split: two workgroups per pair of images
         return 2 * ((n + 1) // 2)
+    if n >= 4 * ncu:                   # persistent wave-specialised kernel
+        return ncu
     return (n + 1) // 2                # two 8x8 images per 4-wave workgroup (convpair_ga_kernel)
 
 

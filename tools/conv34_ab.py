@@ -1,8 +1,6 @@
-"""Same-process A/B of the conv3+conv4 launch forms at batch B (diagnostic):
-the product's default (qcn_conv3x3_pair_u8s8, NHWC output: the persistent
-pipelined kernel above one image per CU) against the per-image ring pair
-kernel (reached through the same entry with a chunk-major output).  HIP events
-around N back-to-back launches of each, alternating, after a warm-up.
+"""Timing of the conv3+conv4 and conv5+conv6 pair launches at batch B
+(diagnostic; run it once per library variant via QCN_LIB for A/B): HIP
+events around N back-to-back launches of each, alternating, after a warm-up.
 
     python tools/conv34_ab.py [B] [N] [ROUNDS]
 """
@@ -35,14 +33,14 @@ def main():
     a2 = model.buffers(B)["a2"].clone()
     L = model.L
     out_n = torch.empty((B, 8, 8, 128), dtype=torch.uint8, device=dev)
-    out_k = torch.empty((8 * 8 * 128 // 32, B, 32), dtype=torch.uint8, device=dev)
-    forms = {"pipelined": lambda: ops.conv_pair(a2, L[2], L[3], out_n, kmajor=False),
-             "ring_pair": lambda: ops.conv_pair(a2, L[2], L[3], out_k, kmajor=True)}
+    a4 = model.buffers(B)["a4"].clone()
+    out6 = torch.empty((128, B, 32), dtype=torch.uint8, device=dev)
+    forms = {"conv34": lambda: ops.conv_pair(a2, L[2], L[3], out_n, kmajor=False),
+             "conv56": lambda: ops.conv_pair(a4, L[4], L[5], out6, kmajor=True)}
     for f in forms.values():
         for _ in range(20):
             f()
     torch.cuda.synchronize()
-    assert torch.equal(out_n.view(B, -1), ops.from_kmajor(out_k)), "forms disagree"
     res = {k: [] for k in forms}
     for _ in range(R):
         for k, f in forms.items():

@@ -26,6 +26,7 @@ from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    kind = int(sys.argv[2]) if len(sys.argv) > 2 else 0   # 0: conv3+conv4, 1: conv5+conv6
     dev = torch.device("cuda:0")
     fp = torch_ref.reference_fp32_model(0, torch_ref.synthetic_images(64, 1))
     folded = fold_state_dict(fp.state_dict())
@@ -36,17 +37,22 @@ def main():
     a2 = model.buffers(B)["a2"].clone()
     L = model.L
     out = torch.empty((B, 8, 8, 128), dtype=torch.uint8, device=dev)
+    a4 = model.buffers(B)["a4"].clone()
+    out6 = torch.empty((128, B, 32), dtype=torch.uint8, device=dev)
     t0 = time.time()
     n = 0
     while time.time() - t0 < 1.5:
         for _ in range(100):
-            ops.conv_pair(a2, L[2], L[3], out)
+            if kind == 0:
+                ops.conv_pair(a2, L[2], L[3], out)
+            else:
+                ops.conv_pair(a4, L[4], L[5], out6, kmajor=True)
         torch.cuda.synchronize()
         n += 100
     lib = _lib.load()
     nwg = min(B, 256)
     buf = np.zeros((1024, 64), np.uint64)
-    rc = lib.qcn_diag_p34_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_int(1024))
+    rc = lib.qcn_diag_p34_stamps(C.c_int(kind), buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_int(1024))
     assert rc == 0, rc
     s = buf[:nwg].astype(np.int64)
     cnt = int((s[0] != 0).sum())
