@@ -546,4 +546,8 @@ def test_conv_pair_workgroup_shapes_equal_layerwise(dev, mode, n):
     assert torch.equal(a4_p, a4_l)
     if n % 128:   # (n % 128 == 0 writes conv6 chunk-major for the head: checked via the logits)
         assert torch.equal(a6_p, a6_l)
-    assert torch.equal(out_p, out_l)
+    if mode == "static":
+        assert torch.equal(out_p, out_l)
+    else:   # QDQ: the split-K head's fp32 fc2 sums in another order than linear_f32
+        assert (out_p - out_l).abs().max().item() <= 1e-5 * out_l.abs().max().item()
+        assert torch.equal(out_p.argmax(1), out_l.argmax(1))
