@@ -212,15 +212,50 @@ def extract_qmodel(q, per_channel=False):
     return qm
 
 
+REF_ROOT = "/root/reference"
+
+
+def import_reference(module, names):
+    """Import ``names`` from the reference's ``module`` (read-only, from
+    REF_ROOT) or return None when that tree is absent: the cross-checks that
+    run the reference's own classes are opt-in, and the generator still writes
+    the fixtures without them (saying so).  The reference imports torchvision
+    at the top of models/custom_quantization_model.py (:4) and never uses it;
+    the wheel is not installed here, so an empty module stands in for it
+    during the import.  The reference's ``models`` package is imported under
+    its own name and removed from sys.modules afterwards (ours shares it)."""
+    import importlib
+    import types
+    if not os.path.isdir(os.path.join(REF_ROOT, "models")):
+        print(f"note: {REF_ROOT} absent: skipping the cross-check against the reference's {module}")
+        return None
+    saved = {k: v for k, v in sys.modules.items() if k == "models" or k.startswith("models.")}
+    for k in saved:
+        del sys.modules[k]
+    stub = "torchvision" not in sys.modules
+    if stub:
+        sys.modules["torchvision"] = types.ModuleType("torchvision")
+    sys.path.insert(0, REF_ROOT)
+    try:
+        mod = importlib.import_module(module)
+        return [getattr(mod, n) for n in names]
+    finally:
+        sys.path.pop(0)
+        for k in [k for k in sys.modules if k == "models" or k.startswith("models.")]:
+            del sys.modules[k]
+        sys.modules.update(saved)
+        if stub:
+            del sys.modules["torchvision"]
+
+
 def check_restatement_against_reference(sd):
     """Import the reference models (read-only, here only) and check that our
     restated topology and our StaticPTQModel counterpart agree bit-for-bit."""
-    sys.path.insert(0, "/root/reference")
-    try:
-        from models.baseline_model import SimpleConvNet
-        from models.static_ptq_model import StaticPTQModel
-    finally:
-        sys.path.pop(0)
+    got = import_reference("models.baseline_model", ["SimpleConvNet"])
+    got2 = import_reference("models.static_ptq_model", ["StaticPTQModel"])
+    if got is None or got2 is None:
+        return False
+    (SimpleConvNet,), (StaticPTQModel,) = got, got2
     x = torch.from_numpy(tr.synthetic_images(16, 5))
     ref = SimpleConvNet()
     ref.load_state_dict(sd)
@@ -369,7 +404,9 @@ def gen_qdq_config2(batch=256):
         ref = qdq(torch.from_numpy(x)).numpy()
     for h in hooks:
         h.remove()
-    rec = {"batch": np.int64(batch), "x_sha": sha(x), "logits": ref, "argmax": qref.argmax_rows(ref)}
+    pinned = reference_qdq_simpleconvnet(fp.state_dict(), [torch.from_numpy(calib)], x, outs, ref)
+    rec = {"batch": np.int64(batch), "x_sha": sha(x), "logits": ref, "argmax": qref.argmax_rows(ref),
+           "pinned_to_reference_class": np.int64(bool(pinned))}
     for i in range(2, 7):   # our a_{i-1} = conv_{i-1}'s QDQ hand-off = conv_i's quantized input
         o = outs[f"in{i}"].int_repr().permute(0, 2, 3, 1).contiguous().numpy()
         rec[f"a{i - 1}_sha"] = sha(o)
@@ -377,6 +414,71 @@ def gen_qdq_config2(batch=256):
     rec["fc1_sha"] = sha(outs["fc1"].int_repr().numpy())
     np.savez_compressed(os.path.join(OUT, "net_qdq_b256.npz"), **rec)
     return rec
+
+
+def reference_qdq_simpleconvnet(state_dict, calib_batches, x, outs, logits):
+    """Pin the config-2 restatement (torch_ref._QDQNet) to the reference's own
+    CustomQuantizationModel / CustomQuantizedSimpleConvNet
+    (/root/reference/models/custom_quantization_model.py:145-261), imported
+    read-only: the same state_dict, CustomQuantizationModel.quantize() (its
+    conv+bn / fc1+bn7 fusion, :169-195), a qconfig on every
+    CustomQuantizedConv2d / CustomQuantizedLinear (their QuantStub -> op ->
+    DeQuantStub run live; the outer stubs :205-206 carry none and stay
+    identities), MinMax calibration on the same batches, then
+    convert.  Every per-layer stub's quantized tensor, fc1's u8 output and the
+    logits must equal _QDQNet's (``outs``, ``logits``) bit for bit.
+
+    The reference's forward flattens with ``x.view(-1, 256 * 4 * 4)`` (:255),
+    which fails on the channels-last tensor its quantized convs hand back; the
+    harness therefore wraps ``pool3`` so its output is made contiguous (a copy,
+    values unchanged) — nothing else in the reference's code path is touched.
+    Returns False (and writes the fixture unpinned) when /root/reference is
+    absent."""
+    import torch.nn as nn
+    import torch.ao.quantization as tq
+    got = import_reference("models.custom_quantization_model",
+                           ["CustomQuantizationModel", "CustomQuantizedConv2d", "CustomQuantizedLinear"])
+    if got is None:
+        return False
+    CustomQuantizationModel, CustomQuantizedConv2d, CustomQuantizedLinear = got
+    torch.backends.quantized.engine = "fbgemm"
+    cm = CustomQuantizationModel()
+    cm.load_state_dict(state_dict)
+    net = cm.quantize().eval()
+    for m in net.modules():
+        if isinstance(m, (CustomQuantizedConv2d, CustomQuantizedLinear)):
+            m.qconfig = tr.static_qconfig(False)
+
+    class _Contig(nn.Module):
+        def __init__(self, pool):
+            super().__init__()
+            self.pool = pool
+
+        def forward(self, t):
+            return self.pool(t).contiguous()
+
+    net.pool3 = _Contig(net.pool3)
+    tq.prepare(net, inplace=True)
+    with torch.no_grad():
+        for xb in calib_batches:
+            net(xb)
+    tq.convert(net, inplace=True)
+    got_outs = {}
+    hooks = [getattr(net, f"conv{i}").quant.register_forward_hook(
+        lambda m, a, o, k=i: got_outs.__setitem__(f"in{k}", o)) for i in range(1, 7)]
+    hooks.append(net.fc1.quant.register_forward_hook(lambda m, a, o: got_outs.__setitem__("in_fc1", o)))
+    hooks.append(net.fc1.linear.register_forward_hook(lambda m, a, o: got_outs.__setitem__("fc1", o)))
+    with torch.no_grad():
+        ref_logits = net(torch.from_numpy(x)).numpy()
+    for h in hooks:
+        h.remove()
+    for k in [f"in{i}" for i in range(1, 7)] + ["in_fc1", "fc1"]:
+        a, b = got_outs[k], outs[k]
+        assert a.q_scale() == b.q_scale() and a.q_zero_point() == b.q_zero_point(), f"{k}: qparams"
+        assert torch.equal(a.int_repr(), b.int_repr()), f"{k}: _QDQNet differs from CustomQuantizedSimpleConvNet"
+    assert ref_logits.dtype == logits.dtype and (ref_logits == logits).all(), "config-2 logits"
+    print("config 2: _QDQNet equals the reference's CustomQuantizedSimpleConvNet at every stub and in the logits")
+    return True
 
 
 # ------------------------------------------- SURVEY §8(f)2 (ResNet blocks)
@@ -589,31 +691,16 @@ def reference_resnet_qdq(fp, calib_batches, per_channel=True):
     convert.  The outer QuantStub / DeQuantStub (:107-108) carry no qconfig
     and stay identities, as in RefQDQResNet.
 
-    That module imports torchvision at the top (:4) and never uses it; the
-    wheel is not installed here, so an empty module object stands in for it
-    during the import.  The reference's `models` package is
-    imported under its own name and removed from sys.modules afterwards."""
+    Imported through import_reference (None when /root/reference is absent:
+    the caller then skips this pin)."""
     import copy
-    import types
     import torch.nn as nn
     import torch.ao.quantization as tq
-    saved = {k: v for k, v in sys.modules.items() if k == "models" or k.startswith("models.")}
-    for k in saved:
-        del sys.modules[k]
-    stub = "torchvision" not in sys.modules
-    if stub:
-        sys.modules["torchvision"] = types.ModuleType("torchvision")
-    sys.path.insert(0, "/root/reference")
-    try:
-        from models.custom_quantization_model import (CustomQuantizedConv2d, CustomQuantizedLinear,
-                                                      CustomQuantizedResNet50)
-    finally:
-        sys.path.pop(0)
-        for k in [k for k in sys.modules if k == "models" or k.startswith("models.")]:
-            del sys.modules[k]
-        sys.modules.update(saved)
-        if stub:
-            del sys.modules["torchvision"]
+    got = import_reference("models.custom_quantization_model",
+                           ["CustomQuantizedConv2d", "CustomQuantizedLinear", "CustomQuantizedResNet50"])
+    if got is None:
+        return None
+    CustomQuantizedConv2d, CustomQuantizedLinear, CustomQuantizedResNet50 = got
     net = copy.deepcopy(fp).eval()
     for li in range(1, 5):   # torchvision Bottleneck attributes the wrapper reads (:63-71)
         for b in getattr(net, f"layer{li}"):
@@ -677,21 +764,22 @@ def gen_resnet_qdq_net(layers=(1, 1, 1, 1), hw=64, n=8, num_classes=10):
     # pin the restatement to the reference's own classes: same fp32 net, same
     # calibration -> every block's fp32 output and the logits bit for bit
     ref = reference_resnet_qdq(fp, [torch.from_numpy(calib)])
-    ref_outs, hooks = {}, []
-    bi = 0
-    for li in range(1, 5):
-        for blk in getattr(ref, f"layer{li}"):
-            hooks.append(blk.register_forward_hook(
-                lambda m, a, o, key=f"block{bi}": ref_outs.__setitem__(key, o)))
-            bi += 1
-    with torch.no_grad():
-        ref_logits = ref(torch.from_numpy(x)).numpy()
-    for h in hooks:
-        h.remove()
-    assert ref_logits.dtype == logits.dtype and (ref_logits == logits).all(), \
-        "RefQDQResNet differs from the reference's CustomQuantizedResNet50"
-    for k, t in ref_outs.items():
-        assert torch.equal(t, outs[k]), f"{k}: RefQDQBottleneck differs from CustomQuantizedBottleneck"
+    if ref is not None:
+        ref_outs, hooks = {}, []
+        bi = 0
+        for li in range(1, 5):
+            for blk in getattr(ref, f"layer{li}"):
+                hooks.append(blk.register_forward_hook(
+                    lambda m, a, o, key=f"block{bi}": ref_outs.__setitem__(key, o)))
+                bi += 1
+        with torch.no_grad():
+            ref_logits = ref(torch.from_numpy(x)).numpy()
+        for h in hooks:
+            h.remove()
+        assert ref_logits.dtype == logits.dtype and (ref_logits == logits).all(), \
+            "RefQDQResNet differs from the reference's CustomQuantizedResNet50"
+        for k, t in ref_outs.items():
+            assert torch.equal(t, outs[k]), f"{k}: RefQDQBottleneck differs from CustomQuantizedBottleneck"
     spec = _resnet_qdq_spec_from_torchao(q)
     mine, inter = qref.resnet_qdq_forward(x, spec, keep=True)
     nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().numpy()  # noqa: E731

@@ -157,3 +157,12 @@ def test_stem_rows_equal_stem_conv():
     rows = qref.stem_pack(x, s, zp)
     acc = qref.conv_acc_nhwc(rows, zp, stem_weight_rows(w), (2, 1), (3, 0))
     assert np.array_equal(acc, acc_ref)
+
+
+def test_config2_fixture_pinned_to_reference_class(golden_dir):
+    """net_qdq_b256.npz was written after oracle/make_golden.py checked the
+    restated _QDQNet against the reference's own CustomQuantizedSimpleConvNet
+    (every per-layer stub, fc1's u8 output and the logits bit for bit;
+    make_golden.reference_qdq_simpleconvnet)."""
+    z = np.load(os.path.join(golden_dir, "net_qdq_b256.npz"))
+    assert int(z["pinned_to_reference_class"]) == 1
