@@ -70,11 +70,12 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
-                  # (the persistent wave-specialised kernel above one image per CU,
-                  # the 8-wave one-image pair kernel at or below)
-                  "conv34": ("conv34ws_kernel", "convpair_kernel<qcn::ConvCfg<64, 128"),
+                  # (the persistent wave-specialised kernel from two images per CU
+                  # (four for conv5+6), the per-tile pair kernels below)
+                  "conv34": ("convpair_ws_kernel<qcn::ConvCfg<64, 128", "convpair_kernel<qcn::ConvCfg<64, 128"),
                   # (one form runs per batch size: the split form at <= 1 image per CU)
-                  "conv56": ("convpair_ga_kernel", "convpair_ga_split_kernel"),
+                  "conv56": ("convpair_ws_kernel<qcn::ConvCfg<128, 256", "convpair_ga_kernel",
+                             "convpair_ga_split_kernel"),
                   # the two-launch head: "fc_finish" matches fc_finish_kernel (static)
                   # and fc_finish_qdq_kernel (QDQ)
                   "fc12": ("fc_splitk_kernel", "fc_finish"),
