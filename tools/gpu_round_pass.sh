@@ -11,8 +11,9 @@ mkdir -p $O
 cd $R
 timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
-timeout -k 10 600 python bench.py --pipeline 2 > $O/bench.json 2> $O/bench.err
-timeout -k 10 300 python bench.py --workload qdq --pipeline 2 > $O/bench_qdq.json 2> $O/bench_qdq.err
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+timeout -k 10 300 python bench.py --no-cpu --no-pmc --pipeline 2 > $O/bench_pipe2.json 2> $O/bench_pipe2.err
+timeout -k 10 300 python bench.py --workload qdq > $O/bench_qdq.json 2> $O/bench_qdq.err
 timeout -k 10 400 python bench.py --workload resnet50 > $O/bench_resnet.json 2> $O/bench_resnet.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- python3 $R/tools/kbench.py 1024 100 > $O/trace.log 2>&1
