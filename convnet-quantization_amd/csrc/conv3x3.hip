@@ -26,6 +26,9 @@
 #include "common.hpp"
 #include <type_traits>
 #include <utility>
+#include <algorithm>
+#include <cmath>
+#include "qconvnet_abi.hpp"
 
 // weight-prefetch depth (K-steps) of the wave-specialised pair kernels; D + 1
 // must divide 18 (build-time constant, not a runtime switch)
@@ -118,10 +121,20 @@ struct ConvEpi {
   const float* mult;   // [COUT]
   const int* corr;     // [COUT] (128 - zp_x) * sum_k w[k]
   int zp_y, lo;        // output zero point, lower clamp (zp_y if relu else 0)
-  int qdq;             // 0: write requantized u8; 1: apply qdq_next
+  int qdq;             // 0: write requantized u8; 1: apply qdq_next; 2: as 1, with the
+                       // exact one-fma form below (qdq_affine, set on the host)
   float s1; int z1; float inv2; int z2;
   int kmajor;          // 1: write y as [f / 32][image][32] (f = NHWC flatten index)
+  // qdq == 2: requant + QDQ hand-off of an accumulator with ab = (acc + u v) m is
+  // cvt_pk(med3(fma(rint(ab), qa, qb), glo, ghi)) — zp_y, lo, the dequantize,
+  // ReLU and the next stub's quantize folded into one fma and one med3
+  float qa, qb, glo, ghi;
 };
+
+// the QDQ hand-off after the requant, in the one-fma form (qdq == 2)
+QCN_DEV float qdq_aff_f(float ab, const ConvEpi& ep) {
+  return __builtin_amdgcn_fmed3f(__builtin_fmaf(__builtin_rintf(ab), ep.qa, ep.qb), ep.glo, ep.ghi);
+}
 
 // Requantize one 32(cout) x 32(pixel) accumulator tile (optionally the max of
 // four quadrant tiles) and write it to the LDS output image [pixel][cout]:
@@ -176,12 +189,14 @@ QCN_DEV void stage_epik(const ConvEpi& ep, float* ek, int tid) {
   }
 }
 
-// FAST: zp_y == 0, lo == 0 and no QDQ hand-off (every post-ReLU layer of the
-// static net).  Then clamp(rne(ab) + zp, lo, 255) == v_cvt_pk_u8_f32(ab), which
+// EM (epilogue mode) 1 — FAST: zp_y == 0, lo == 0 and no QDQ hand-off (every
+// post-ReLU layer of the static net).  Then clamp(rne(ab) + zp, lo, 255) == v_cvt_pk_u8_f32(ab), which
 // rounds half-to-even and saturates to [0, 255] (probed exhaustively on gfx950,
 // tools/micro/cvt_probe.hip), and the fma / mul run as packed fp32 pairs:
 // 3 VALU per element instead of 7 (the epilogue is VALU-issue bound).
-template <int NQ, bool XORIN, bool FAST, bool D32 = false, bool GWT = false>
+// EM 2: the QDQ hand-off in its one-fma form (qdq == 2): 6 VALU per element
+// instead of 15.  EM 0: the general requant (+ qdq_next_f).
+template <int NQ, bool XORIN, int EM, bool D32 = false, bool GWT = false>
 QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
                              int hi, uint8_t* orow, const uint8_t* wbase = nullptr, uint32_t woff = 0) {
   // accumulators already include the zero-point correction (acc_init_corr)
@@ -198,7 +213,7 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
       a[e] = accs[0][rg];
       if constexpr (NQ == 4) a[e] = max(max(a[e], accs[1][rg]), max(accs[2][rg], accs[3][rg]));
     }
-    if constexpr (FAST) {
+    if constexpr (EM != 0) {
       // scalar fma / mul (built with -fno-slp-vectorize so they stay scalar):
       // packed fp32 issues slower beside a partner wave's MFMAs
 #pragma unroll
@@ -206,6 +221,7 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
         const int rg = 4 * g + e;
         float f = __builtin_fmaf(K.u[rg], K.v[rg], (float)a[e]);
         f = f * K.m[rg];
+        if constexpr (EM == 2) f = qdq_aff_f(f, ep);
         wd = __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
       }
     } else {
@@ -245,13 +261,15 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
     *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-QCN_DEV bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
+__host__ __device__ inline bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
+inline int epi_mode(const ConvEpi& ep) { return ep.qdq == 2 ? 2 : (epi_fast(ep) ? 1 : 0); }
 
 template <int NQ, bool XORIN = false, bool D32 = false, bool GWT = false>
 QCN_DEV void epilogue_tile_kf(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
                               int hi, uint8_t* orow, const uint8_t* wbase = nullptr, uint32_t woff = 0) {
-  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, true, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
-  else epilogue_tile_k<NQ, XORIN, false, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
+  if (epi_fast(ep)) epilogue_tile_k<NQ, XORIN, 1, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
+  else if (ep.qdq == 2) epilogue_tile_k<NQ, XORIN, 2, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
+  else epilogue_tile_k<NQ, XORIN, 0, D32, GWT>(accs, K, ep, co_base, hi, orow, wbase, woff);
 }
 
 template <int NQ, bool XORIN = false>
@@ -1035,13 +1053,15 @@ QCN_DEV void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// One requantized output into byte e of wd (epilogue_tile_k's arithmetic).
-template <bool FAST>
+// One requantized output into byte e of wd (epilogue_tile_k's arithmetic,
+// EM as there).
+template <int EM>
 QCN_DEV uint32_t rq_elem(int a, const EpiG& K, int e, const ConvEpi& ep, uint32_t wd) {
   const float u = f4e(K.u, e), v = f4e(K.v, e), m = f4e(K.m, e);
-  if constexpr (FAST) {
+  if constexpr (EM != 0) {
     float f = __builtin_fmaf(u, v, (float)a);
     f = f * m;
+    if constexpr (EM == 2) f = qdq_aff_f(f, ep);
     return __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
   } else {
     float q = requant_f(a, u, v, m, (float)ep.zp_y, (float)ep.lo);
@@ -1189,7 +1209,7 @@ struct PairWs {
   static constexpr int OPI = CB::OPX / SEGS;   // pooled output pixels per image
 };
 
-template <class CA, class CB, int D, bool FA, bool FB, bool KMAJOR>
+template <class CA, class CB, int D, int FA, int FB, bool KMAJOR>
 __global__ __launch_bounds__(512, 1)
 void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
                         ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
@@ -1856,7 +1876,10 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       }
     };
     auto rows = [&](auto mode) {
-      constexpr int MODE = decltype(mode)::value;  // 0 general, 1 v+mult uniform, 2 v uniform
+      // 0 general, 1 v+mult uniform, 2 v uniform; 3 / 4: 1 / 2 with the
+      // one-fma QDQ hand-off (ep1.qdq == 2)
+      constexpr int MODE = decltype(mode)::value > 2 ? decltype(mode)::value - 2 : decltype(mode)::value;
+      constexpr bool AFF = decltype(mode)::value > 2;
       // lean epilogue constants: u (and mult unless uniform) of this lane's
       // 16 channels per half; v (and mult) as scalars.  EpiK (96 VGPRs) for
       // the general path only.
@@ -1923,6 +1946,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
               float f = (float)acc[i][e];
               f = __builtin_fmaf(u[i][e], sv, f);
               f = f * (MODE == 1 ? sm : m[i][e]);
+              if constexpr (AFF) f = qdq_aff_f(f, ep1);
               t[i][e >> 1][e & 1] = f;
             }
           uint8_t* prow_ptr = pb + C::slot(0, tr, l32 + 1);
@@ -1966,6 +1990,9 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     if (fast1 && vuni) {
       if (muni) rows(std::integral_constant<int, 1>{});
       else rows(std::integral_constant<int, 2>{});
+    } else if (ep1.qdq == 2 && vuni) {
+      if (muni) rows(std::integral_constant<int, 3>{});
+      else rows(std::integral_constant<int, 4>{});
     } else {
       rows(std::integral_constant<int, 0>{});
     }
@@ -2069,6 +2096,101 @@ __global__ void conv3x3_generic_kernel(const uint8_t* __restrict__ x, int nimg, 
   }
 }
 
+// ---- host: the QDQ hand-off in one fma (ConvEpi::qdq == 2)
+//
+// After the requant the hand-off is a function of one integer only: with
+// r = rint(ab), the layer's u8 output is q1 = clamp(r + zp_y, lo, 255) and the
+// next stub's input g(q1) = clamp(rint(relu((q1 - z1) s1) inv2) + z2, 0, 255)
+// (qdq_next_f's fp32 op order).  g is nondecreasing, so on the 256 values of q1
+// it can be an exact affine map followed by a clamp: find fp32 (qa, qb) with
+// rne(fma(r, qa, qb)) == g(clamp(r + zp_y, lo, 255)) for every r with q1 in
+// [lo, 255] (glo = g(lo), ghi = g(255) clamp the rest: fma is monotone in r
+// for qa > 0), and check every one of those r in the device's fp32
+// arithmetic.  Layers for which no candidate passes keep the general path.
+namespace {
+
+#pragma clang fp contract(off)
+float qdq_ref_host(float q1, const ConvEpi& ep) {
+  float x = (q1 - (float)ep.z1) * ep.s1;
+  x = x > 0.0f ? x : 0.0f;
+  const float t = std::fmin(x * ep.inv2, 1.0e9f);
+  const float r = std::nearbyint(t) + (float)ep.z2;
+  return std::fmin(std::fmax(r, 0.0f), 255.0f);
+}
+
+float rne_sat_u8(float x) {   // v_cvt_pk_u8_f32: round half to even, saturate
+  const float r = std::nearbyint(x);
+  return std::fmin(std::fmax(r, 0.0f), 255.0f);
+}
+
+bool qdq_affine_solve(ConvEpi& ep) {
+  const int zp = ep.zp_y, lo = ep.lo;
+  const int r0 = lo - zp, r1 = 255 - zp;
+  if (r0 > r1) return false;
+  auto g = [&](int r) {
+    const float q1 = std::fmin(std::fmax((float)r + (float)zp, (float)lo), 255.0f);
+    return qdq_ref_host(q1, ep);
+  };
+  const float glo = g(r0), ghi = g(r1);
+  const double c = (double)ep.s1 * (double)ep.inv2;
+  if (!(c > 0.0) || !std::isfinite(c)) return false;
+  for (int k = 0; k < 81; ++k) {   // qa = c (1 + d), d = 0, -1e-7, +1e-7, -2e-7, ...
+    const double d = ((k + 1) / 2) * 1.0e-7 * ((k & 1) ? -1.0 : 1.0);
+    const float qa = (float)(c * (1.0 + d));
+    if (!(qa > 0.0f)) continue;
+    double lb = -1.0e30, ub = 1.0e30;
+    for (int r = r0; r <= r1; ++r) {
+      const double gr = g(r), ar = (double)qa * r;
+      if (gr > glo) lb = std::max(lb, gr - 0.5 - ar);
+      if (gr < ghi) ub = std::min(ub, gr + 0.5 - ar);
+    }
+    double mid;
+    if (lb > -1.0e29 && ub < 1.0e29) mid = 0.5 * (lb + ub);
+    else if (lb > -1.0e29) mid = lb + 0.25;
+    else if (ub < 1.0e29) mid = ub - 0.25;
+    else mid = (double)glo;
+    if (!(lb < ub)) continue;
+    const float qb = (float)mid;
+    bool ok = true;
+    for (int r = r0; r <= r1 && ok; ++r) {
+      const float v = std::fmin(std::fmax(std::fma((float)r, qa, qb), glo), ghi);
+      ok = rne_sat_u8(v) == g(r);
+    }
+    if (ok) {
+      ep.qa = qa; ep.qb = qb; ep.glo = glo; ep.ghi = ghi;
+      return true;
+    }
+  }
+  return false;
+}
+#pragma clang fp contract(on)
+
+}  // namespace
+
+// The QDQ hand-off of qcn_qdq_t q into ep (ep.zp_y / ep.lo already set):
+// qdq = 2 with the one-fma constants when an exact form exists, else 1.
+// Solved once per distinct (layer qparams, next stub) and cached.
+void set_qdq(ConvEpi& ep, const qcn_qdq_t* q) {
+  ep.qdq = 1;
+  ep.s1 = q->s1; ep.z1 = q->z1; ep.inv2 = q->inv2; ep.z2 = q->z2;
+  struct Entry { float s1, inv2; int z1, z2, zp, lo; bool ok; float qa, qb, glo, ghi; };
+  static thread_local Entry cache[16];
+  static thread_local int ncache = 0, next = 0;
+  for (int i = 0; i < ncache; ++i) {
+    const Entry& e = cache[i];
+    if (e.s1 == ep.s1 && e.inv2 == ep.inv2 && e.z1 == ep.z1 && e.z2 == ep.z2 && e.zp == ep.zp_y &&
+        e.lo == ep.lo) {
+      if (e.ok) { ep.qdq = 2; ep.qa = e.qa; ep.qb = e.qb; ep.glo = e.glo; ep.ghi = e.ghi; }
+      return;
+    }
+  }
+  const bool ok = qdq_affine_solve(ep);
+  if (ok) ep.qdq = 2;
+  cache[next] = Entry{ep.s1, ep.inv2, ep.z1, ep.z2, ep.zp_y, ep.lo, ok, ep.qa, ep.qb, ep.glo, ep.ghi};
+  next = (next + 1) % 16;
+  if (ncache < 16) ++ncache;
+}
+
 }  // namespace qcn
 
 // ==========================================================================
@@ -2119,7 +2241,7 @@ int launch_pair_ga(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-template <class CA, class CB, int D, bool FA, bool FB, bool KM>
+template <class CA, class CB, int D, int FA, int FB, bool KM>
 int launch_pair_ws_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
                      const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
   using P = PairWs<CA, CB, D>;
@@ -2135,14 +2257,16 @@ int launch_pair_ws_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, con
 template <class CA, class CB, int D>
 int launch_pair_ws(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
                    const int8_t* wb, const ConvEpi& epb, bool kmajor, uint8_t* y, hipStream_t st, int ncu) {
-  // the FBGEMM fast path (zp_y == 0, no floor, no QDQ hand-off) is known on the host
-  const bool fa = epa.zp_y == 0 && epa.lo == 0 && epa.qdq == 0;
-  const bool fb = epb.zp_y == 0 && epb.lo == 0 && epb.qdq == 0;
+  // epilogue modes, known on the host: 1 the FBGEMM fast path (zp_y == 0, no
+  // floor, no QDQ hand-off), 2 the one-fma QDQ form (both convs: the QDQ
+  // net), 0 general
+  int fa = epi_mode(epa), fb = epi_mode(epb);
+  if ((fa == 2) != (fb == 2)) { fa = fa == 2 ? 0 : fa; fb = fb == 2 ? 0 : fb; }
 #define QCN_WS(FA_, FB_, KM_) \
   if (fa == FA_ && fb == FB_ && kmajor == KM_)                                                            \
     return launch_pair_ws_k<CA, CB, D, FA_, FB_, KM_>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
-  QCN_WS(true, true, false) QCN_WS(true, false, false) QCN_WS(false, true, false) QCN_WS(false, false, false)
-  QCN_WS(true, true, true) QCN_WS(true, false, true) QCN_WS(false, true, true) QCN_WS(false, false, true)
+  QCN_WS(1, 1, false) QCN_WS(1, 0, false) QCN_WS(0, 1, false) QCN_WS(0, 0, false) QCN_WS(2, 2, false)
+  QCN_WS(1, 1, true) QCN_WS(1, 0, true) QCN_WS(0, 1, true) QCN_WS(0, 0, true) QCN_WS(2, 2, true)
 #undef QCN_WS
   return QCN_ERR_UNSUPPORTED;
 }
@@ -2254,6 +2378,17 @@ int qcn_pack_conv1_weight(const int8_t* w_oihw, int cout, int8_t* out, int32_t* 
   return QCN_OK;
 }
 
+int qcn_qdq_affine(const qcn_qdq_t* q, int y_zp, int lo, float* out) {
+  if (!q || !out || y_zp < 0 || y_zp > 255 || lo < 0 || lo > 255) return QCN_ERR_ARG;
+  qcn::ConvEpi ep{};
+  ep.zp_y = y_zp;
+  ep.lo = lo;
+  qcn::set_qdq(ep, q);
+  if (ep.qdq != 2) return 0;
+  out[0] = ep.qa; out[1] = ep.qb; out[2] = ep.glo; out[3] = ep.ghi;
+  return 1;
+}
+
 int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
                           const int8_t* wa_packed, int cmid, const float* ua, const float* va,
                           const float* multa, const int32_t* corra, int zmid, int relua,
@@ -2269,16 +2404,12 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   ConvEpi epa{ua, va, multa, corra, zmid, relua ? zmid : 0, 0, 0.f, 0, 0.f, 0, 0};
   int xb_zp = zmid;
   if (qdqa) {
-    epa.qdq = 1;
-    epa.s1 = qdqa->s1; epa.z1 = qdqa->z1; epa.inv2 = qdqa->inv2; epa.z2 = qdqa->z2;
+    qcn::set_qdq(epa, qdqa);
     xb_zp = qdqa->z2;
   }
   if (kmajor && (long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
   ConvEpi epb{ub, vb, multb, corrb, y_zp, relub ? y_zp : 0, 0, 0.f, 0, 0.f, 0, kmajor ? 1 : 0};
-  if (qdqb) {
-    epb.qdq = 1;
-    epb.s1 = qdqb->s1; epb.z1 = qdqb->z1; epb.inv2 = qdqb->inv2; epb.z2 = qdqb->z2;
-  }
+  if (qdqb) qcn::set_qdq(epb, qdqb);
   hipStream_t st = (hipStream_t)stream;
   using namespace qcn;
   // wave tile: 64 couts x 128 pixels, two waves per SIMD (two workgroups per
@@ -2348,10 +2479,7 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
   if (x_zp < 0 || x_zp > 255 || y_zp < 0 || y_zp > 255) return QCN_ERR_ARG;
   if (pool && ((h & 1) || (w & 1))) return QCN_ERR_ARG;
   ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
-  if (qdq) {
-    ep.qdq = 1;
-    ep.s1 = qdq->s1; ep.z1 = qdq->z1; ep.inv2 = qdq->inv2; ep.z2 = qdq->z2;
-  }
+  if (qdq) qcn::set_qdq(ep, qdq);
   hipStream_t st = (hipStream_t)stream;
   if (h == w && cin % 64 == 0 && cout % 64 == 0) {
     const int rc = dispatch_conv(cin, cout, h, pool, x, nimg, x_zp, w_packed, ep, y, st);
@@ -2379,9 +2507,9 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
       y_zp < 0 || y_zp > 255 || z1 < 0 || z1 > 255)
     return QCN_ERR_ARG;
   ConvEpi ep1{u1, v1, mult1, corr1, z1, relu1 ? z1 : 0, 0, 0.f, 0, 0.f, 0, 0};
-  if (qdq1) { ep1.qdq = 1; ep1.s1 = qdq1->s1; ep1.z1 = qdq1->z1; ep1.inv2 = qdq1->inv2; ep1.z2 = qdq1->z2; }
+  if (qdq1) qcn::set_qdq(ep1, qdq1);
   ConvEpi ep2{u2, v2, mult2, corr2, y_zp, relu2 ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
-  if (qdq2) { ep2.qdq = 1; ep2.s1 = qdq2->s1; ep2.z1 = qdq2->z1; ep2.inv2 = qdq2->inv2; ep2.z2 = qdq2->z2; }
+  if (qdq2) qcn::set_qdq(ep2, qdq2);
   static bool attr_done[QCN_MAX_DEV] = {};
   static int ncu_dev[QCN_MAX_DEV] = {};
   if (!qcn_set_lds_once((const void*)qcn::conv12p_kernel, qcn::Conv12P::LDS, attr_done))
@@ -2407,10 +2535,7 @@ int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_
   if (!x || !w1_packed || !u || !v || !mult || !corr || !y) return QCN_ERR_ARG;
   if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
   ConvEpi ep{u, v, mult, corr, y_zp, relu ? y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
-  if (qdq) {
-    ep.qdq = 1;
-    ep.s1 = qdq->s1; ep.z1 = qdq->z1; ep.inv2 = qdq->inv2; ep.z2 = qdq->z2;
-  }
+  if (qdq) qcn::set_qdq(ep, qdq);
   const float inv = 1.0f / in_scale;
   hipStream_t st = (hipStream_t)stream;
   const long pix = (long)nimg * hw * hw;

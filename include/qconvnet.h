@@ -171,6 +171,16 @@ int qcn_linear_u8s8(const uint8_t* x, int m, int k, int x_zp, const int8_t* w, i
 long long qcn_classifier_workspace_size(int m, int n1);
 /* Host: s8 [n][k] row-major -> [k/32][n][32] (k % 32 == 0). */
 int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out);
+/* Host: the QDQ hand-off (qcn_qdq_t) after a requant to (y_zp, lo) in its
+ * one-fma form.  With r = rint(ab) of the requant, the layer output is
+ * q1 = clamp(r + y_zp, lo, 255) and the next stub's input g(q1); on success
+ * (returns 1) out[4] = {qa, qb, glo, ghi} with
+ *   g(clamp(r + y_zp, lo, 255)) == rne_sat_u8(med3(fma(r, qa, qb), glo, ghi))
+ * for every integer r (checked in fp32 over all r with q1 in [lo, 255]);
+ * returns 0 when no exact form was found (the conv epilogues then run the
+ * general requant + qdq sequence).  The conv launchers apply it themselves;
+ * exported for the host tests (no device work). */
+int qcn_qdq_affine(const qcn_qdq_t* q, int y_zp, int lo, float* out);
 int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1, const float* u1,
                         const float* v1, const float* mult1, const int32_t* corr1, int y1_zp,
                         int relu1, const int8_t* w2, int n2, const float* u2, const float* v2,

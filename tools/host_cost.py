@@ -16,8 +16,8 @@ dev = torch.device("cuda:0")
 fp = torch_ref.reference_fp32_model(0, torch_ref.synthetic_images(64, 1))
 folded = fold_state_dict(fp.state_dict())
 ranges = calibrate(folded, [torch.from_numpy(torch_ref.synthetic_images(64, 1))], "cpu")
-model = QuantizedConvNet(build_qspec(folded, ranges, "static"), dev)
-for B in (128, 1024):
+for mode, B in (("static", 128), ("static", 256), ("qdq", 256), ("static", 1024)):
+    model = QuantizedConvNet(build_qspec(folded, ranges, mode), dev)
     x = torch.from_numpy(torch_ref.synthetic_images(B, 0)).to(dev)
     for _ in range(20):
         model.run(x)
@@ -38,5 +38,5 @@ for B in (128, 1024):
         model.replay(B)
     torch.cuda.synchronize()
     t_g = time.perf_counter() - t0
-    print(f"batch {B}: eager {t_all / n * 1e6:.1f} us/step (host issue {t_host / n * 1e6:.1f} us/step), "
+    print(f"{mode} batch {B}: eager {t_all / n * 1e6:.1f} us/step (host issue {t_host / n * 1e6:.1f} us/step), "
           f"graph replay {t_g / n * 1e6:.1f} us/step", flush=True)

@@ -2,7 +2,7 @@
 baselines): random-init SimpleConvNet (BN recalibrated), calibrated on 64
 synthetic images, then ITERS forwards at batch B on cuda:0.
 
-    python tools/kbench.py [B] [ITERS]
+    python tools/kbench.py [B] [ITERS] [MODE]     (MODE: static | qdq)
 
 Under rocprofv3 every dispatch is one of the product kernels, so PMC passes
 (e.g. GRBM_GUI_ACTIVE for the effective clock) are not diluted by the
@@ -26,11 +26,12 @@ from qconvnet.qmodel import QuantizedConvNet, build_qspec, calibrate, fold_state
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    mode = sys.argv[3] if len(sys.argv) > 3 else "static"
     dev = torch.device("cuda:0")
     fp = torch_ref.reference_fp32_model(0, torch_ref.synthetic_images(64, 1))
     folded = fold_state_dict(fp.state_dict())
     ranges = calibrate(folded, [torch.from_numpy(torch_ref.synthetic_images(64, 1))], "cpu")
-    model = QuantizedConvNet(build_qspec(folded, ranges, "static"), dev)
+    model = QuantizedConvNet(build_qspec(folded, ranges, mode), dev)
     x = torch.from_numpy(torch_ref.synthetic_images(B, 0)).to(dev)
     for _ in range(5):
         model.run(x)
