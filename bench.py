@@ -54,6 +54,7 @@ MAC_PER_IMAGE["fc12"] = MAC_PER_IMAGE["fc1"] + MAC_PER_IMAGE["fc2"]
 MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
 MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
 MAC_PER_IMAGE["net"] = sum(MAC_PER_IMAGE[f"conv{i}"] for i in range(1, 7))
+MAC_PER_IMAGE["conv1_6"] = MAC_PER_IMAGE["net"]   # the one-launch conv1 .. conv6
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -66,10 +67,14 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "fc12": 4096 + 512 + 10 + 40,
                  "conv34": 16 * 16 * 64 + 8 * 8 * 128,
                  "conv56": 8 * 8 * 128 + 4 * 4 * 256,
-                 "net": 3 * 32 * 32 * 4 + 4 * 4 * 256}
+                 "net": 3 * 32 * 32 * 4 + 4 * 4 * 256,
+                 # one launch: fp32 input, a6 out, and the a2 / a4 hand-offs it
+                 # writes and reads back through memory
+                 "conv1_6": 3 * 32 * 32 * 4 + 4 * 4 * 256 + 2 * (16 * 16 * 64 + 8 * 8 * 128)}
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
-KERNEL_SYMBOLS = {"conv12": ("conv12p_kernel",),
+KERNEL_SYMBOLS = {"conv1_6": ("convnet_convs_kernel",),
+                  "conv12": ("conv12p_kernel",),
                   # (the persistent wave-specialised kernel from two images per CU
                   # (four for conv5+6), the per-tile pair kernels below)
                   "conv34": ("convpair_ws_kernel<qcn::ConvCfg<64, 128", "convpair_kernel<qcn::ConvCfg<64, 128"),
@@ -479,7 +484,10 @@ def pmc_counters(model, sd, args, names, timeout=150):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps K (default 400 for the SimpleConvNet workloads, 50 for "
+                         "ResNet-50: each timed region pays ~0.15-0.2 ms of start-up after its "
+                         "synchronize, 2-4 %% of a 50-step region of 0.07-0.14 ms steps)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--warmup-min-ms", type=float, default=WARMUP_MIN_S * 1e3,
                     help="after the W warmup steps, keep running untimed forwards until this many ms "
@@ -510,6 +518,8 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = {"convnet": 1024, "qdq": 256, "resnet50": 512}[args.workload]
+    if args.steps is None:
+        args.steps = 50 if args.workload == "resnet50" else 400
     if args.workload == "resnet50":
         return main_resnet(args)
 

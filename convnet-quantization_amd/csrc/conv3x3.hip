@@ -1209,11 +1209,14 @@ struct PairWs {
   static constexpr int OPI = CB::OPX / SEGS;   // pooled output pixels per image
 };
 
-template <class CA, class CB, int D, int FA, int FB, bool KMAJOR>
-__global__ __launch_bounds__(512, 1)
-void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
-                        ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
-                        uint8_t* __restrict__ y) {
+// Workgroup b of G: its tiles are k = 0 .. T-1.  Image of segment s of tile k:
+// (b + k G) SEGS + s (ILV = false: tile b + k G of the batch), or
+// b + (k SEGS + s) G (ILV = true: the images b, b + G, b + 2G, ... that the
+// earlier phases of convnet_convs_kernel gave this workgroup, paired up).
+template <class CA, class CB, int D, int FA, int FB, bool KMAJOR, bool ILV = false>
+QCN_DEV void convpair_ws_body(int b, int G, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                              const int8_t* __restrict__ wa, const ConvEpi& epa, int xb_zp,
+                              const int8_t* __restrict__ wb, const ConvEpi& epb, uint8_t* __restrict__ y) {
   using P = PairWs<CA, CB, D>;
   constexpr int SEGS = P::SEGS, IMG = CA::IMG, W = CA::W, WCO = CA::WCO;
   constexpr int CH16 = CA::kCin / 16;
@@ -1222,20 +1225,26 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
   const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // 0: conv A, 1: conv B
   const int rt = tid & 255, lane = tid & 63, wave = rt >> 6;   // thread / wave within the role
   const int wc = wave % WCO, wp = wave / WCO;
-  const int b = (int)blockIdx.x, G = (int)gridDim.x;
-  const int ntile = (nimg + SEGS - 1) / SEGS;
-  const int T = b < ntile ? (ntile - 1 - b) / G + 1 : 0;   // this workgroup's tiles b, b + G, ...
+  int T;
+  if constexpr (ILV) {
+    const int mine = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // images b, b + G, ...
+    T = (mine + SEGS - 1) / SEGS;
+  } else {
+    const int ntile = (nimg + SEGS - 1) / SEGS;
+    T = b < ntile ? (ntile - 1 - b) / G + 1 : 0;   // this workgroup's tiles b, b + G, ...
+  }
+  auto img_of = [&](int k, int sg) { return ILV ? b + (k * SEGS + sg) * G : (b + k * G) * SEGS + sg; };
 #ifdef QCN_PIPE34_STAMP
   int stamp_i = 0;
   constexpr int stamp_kind = CA::kCin == 64 ? 0 : 1;
   if (threadIdx.x < 64) p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
   P34_STAMP();
-  // tile t's input piece q of this A-role thread (images past the batch read
+  // tile k's input piece q of this A-role thread (images past the batch read
   // the last image: their outputs are never stored)
-  auto in_src = [&](int t, int q) {
+  auto in_src = [&](int k, int q) {
     const int p = rt + 256 * q;
-    int n = t * SEGS + p / (IMG * CH16);
+    int n = img_of(k, p / (IMG * CH16));
     n = n < nimg ? n : nimg - 1;
     return x + ((long)n * IMG + (p / CH16) % IMG) * CA::kCin + (p % CH16) * 16;
   };
@@ -1248,7 +1257,7 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
   uint4 sv[4];
   if (role == 0 && T > 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(b, q));
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(0, q));
   }
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
@@ -1390,8 +1399,8 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
   };
   // B's pooled epilogue of acc for tile t (max over the four quadrant tiles,
   // requant, two permlane32 swap rounds, one 16-B store per tile row and lane)
-  auto epi_b = [&](const Lane& L, int t) {
-    const int n = t * SEGS + L.q / P::OPI, pix = L.q % P::OPI;
+  auto epi_b = [&](const Lane& L, int k) {
+    const int n = img_of(k, L.q / P::OPI), pix = L.q % P::OPI;
     static_for<2>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       EpiG K[4];
@@ -1442,9 +1451,9 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
         pipe_job<CA, D, true>(pa_buf(p), L.ca, wra, wra, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
         // tile p + 1 (a valid dummy past the last): loads now, written after the
         // epilogue (double A patch) or after the next period barrier
-        const int tn = b + (p + 1 < T ? p + 1 : p) * G;
+        const int kn = p + 1 < T ? p + 1 : p;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(tn, q));
+        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(kn, q));
         epi_a(L, pb_buf(p));
         if constexpr (P::DOUBLE_A) write_in(pa_buf(p + 1));
       }
@@ -1458,7 +1467,7 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
       if constexpr (!P::DOUBLE_A) lds_barrier();
       if (p >= 1) {
         const Lane L = lanes();
-        if (p >= 2) epi_b(L, b + (p - 2) * G);
+        if (p >= 2) epi_b(L, p - 2);
         pipe_job<CB, D, true>(pb_buf(p - 1), L.cb, wrb, wrb, voff, wc, wp, L.l32, L.hi, acc, ga, nofill);
       }
       P34_STAMP();
@@ -1466,12 +1475,21 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
       P34_STAMP();
     }
     const Lane L = lanes();
-    epi_b(L, b + (T - 1) * G);
+    epi_b(L, T - 1);
   }
   P34_STAMP();
 #ifdef QCN_PIPE34_STAMP
   if (threadIdx.x < 64) p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
+}
+
+template <class CA, class CB, int D, int FA, int FB, bool KMAJOR>
+__global__ __launch_bounds__(512, 1)
+void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
+                        ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
+                        uint8_t* __restrict__ y) {
+  convpair_ws_body<CA, CB, D, FA, FB, KMAJOR>((int)blockIdx.x, (int)gridDim.x, x, nimg, x_zp, wa, epa, xb_zp,
+                                              wb, epb, y);
 }
 
 // --------------------------------------------------------------------------
@@ -2056,6 +2074,56 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
 }
 
 // --------------------------------------------------------------------------
+// conv1 .. conv6 in ONE persistent launch (r04).  Every conv of the net reads
+// only its own image, and the three persistent kernels of the forward give
+// workgroup b of G the same images b, b + G, b + 2G, ... (conv12p: whole
+// images, top half then bottom half; the conv3+4 pair: one image per tile;
+// the conv5+6 pair: two images per tile, paired as b + 2kG, b + (2k+1)G
+// here).  So the workgroup runs the three phases back to back over its own
+// images with no cross-workgroup dependency: the two dependent-launch
+// boundaries (a kernel's drain, the next one's dispatch ramp and prologue)
+// go away.  a2 / a4 pass through memory as before (write-through stores,
+// drained before the phase barrier; this CU never read those addresses
+// before in this launch, so its L1 holds no stale copy).  Same LDS, same
+// numerics, same code as the three launches (phase bodies shared).
+struct ConvnetLayers {
+  const int8_t* w[6];
+  ConvEpi ep[6];
+  int x_zp[6];   // input zero point of conv i (x_zp[0]: the QuantStub's)
+};
+
+using WsA3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
+using WsB4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+using WsA5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
+using WsB6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE34_D>::LDS,
+                                                   PairWs<WsA5, WsB6, QCN_PIPE34_D>::LDS));
+
+QCN_DEV void phase_boundary() {
+  // every wave's stores of the phase complete, all LDS use done, default priority
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_setprio(0);
+  __syncthreads();
+}
+
+template <int EM, bool KMAJOR>
+__global__ __launch_bounds__(512, 1)
+void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, ConvnetLayers L,
+                          uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
+  const int b = (int)blockIdx.x, G = (int)gridDim.x;
+  const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
+  conv12p_body(b, G, T, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1], a2);
+  phase_boundary();
+  convpair_ws_body<WsA3, WsB4, QCN_PIPE34_D, EM, EM, false>(b, G, a2, nimg, L.x_zp[2], L.w[2], L.ep[2],
+                                                            L.x_zp[3], L.w[3], L.ep[3], a4);
+  phase_boundary();
+  convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, L.x_zp[4], L.w[4], L.ep[4],
+                                                                   L.x_zp[5], L.w[5], L.ep[5], a6);
+}
+
+// --------------------------------------------------------------------------
 // Generic fallback (any CIN/COUT/H/W, no MFMA): one thread per output element.
 // Used only for shapes without a tuned instantiation (unit tests, odd sizes).
 __global__ void conv3x3_generic_kernel(const uint8_t* __restrict__ x, int nimg, int H, int W,
@@ -2109,7 +2177,6 @@ __global__ void conv3x3_generic_kernel(const uint8_t* __restrict__ x, int nimg, 
 // arithmetic.  Layers for which no candidate passes keep the general path.
 namespace {
 
-#pragma clang fp contract(off)
 float qdq_ref_host(float q1, const ConvEpi& ep) {
   float x = (q1 - (float)ep.z1) * ep.s1;
   x = x > 0.0f ? x : 0.0f;
@@ -2163,7 +2230,6 @@ bool qdq_affine_solve(ConvEpi& ep) {
   }
   return false;
 }
-#pragma clang fp contract(on)
 
 }  // namespace
 
@@ -2426,8 +2492,8 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
       return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
-    using A3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
-    using B4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
+    using A3 = WsA3;
+    using B4 = WsB4;
     // two or more images per CU: the persistent wave-specialised kernel
     if (QCN_WS34 && nimg >= 2 * ncu)
       return launch_pair_ws<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
@@ -2437,8 +2503,8 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
     // two images per 4-wave workgroup, two workgroups per CU, weights from L2
     // into registers 4 K-steps ahead (convpair_ga_kernel)
-    using A1 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
-    using B1 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
+    using A1 = WsA5;
+    using B1 = WsB6;
     // at or below one image per CU, conv6's couts split over two workgroups
     // (conv5 computed by both): twice the workgroups.  Batch 256: 22.3 ->
     // 20.6-21.7 us; batch 512 (one workgroup per CU either way) 27.9 -> 33.3
@@ -2526,6 +2592,54 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
                      (hipStream_t)stream, x, nimg, 1.0f / in_scale, in_zp, w1_packed, ep1, x2_zp,
                      w2_packed, ep2, y);
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
+                               const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
+                               int kmajor, void* stream) {
+  if (!x || !layers || !a2 || !a4 || !a6) return QCN_ERR_ARG;
+  if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
+  qcn::ConvnetLayers L{};
+  for (int i = 0; i < 6; ++i) {
+    const qcn_conv_layer_t& l = layers[i];
+    if (!l.w || !l.u || !l.v || !l.mult || !l.corr) return QCN_ERR_ARG;
+    if (l.x_zp < 0 || l.x_zp > 255 || l.y_zp < 0 || l.y_zp > 255) return QCN_ERR_ARG;
+    L.w[i] = l.w;
+    L.ep[i] = ConvEpi{l.u, l.v, l.mult, l.corr, l.y_zp, l.relu ? l.y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
+    if (l.qdq) qcn::set_qdq(L.ep[i], l.qdq);
+    L.x_zp[i] = l.x_zp;
+  }
+  if (L.x_zp[0] != in_zp) return QCN_ERR_ARG;
+  L.ep[5].kmajor = kmajor ? 1 : 0;
+  if ((long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
+  const int ncu = qcn_cu_count();
+  if (ncu <= 0) return QCN_ERR_HIP;
+  // the two pair phases are the wave-specialised kernels of >= 4 images per CU;
+  // conv3..conv6 all on the FBGEMM fast epilogue or all on the one-fma QDQ form
+  if (nimg < 4 * ncu) return QCN_ERR_UNSUPPORTED;
+  int em = -1;
+  bool all1 = true, all2 = true;
+  for (int i = 2; i < 6; ++i) {
+    all1 = all1 && qcn::epi_mode(L.ep[i]) == 1;
+    all2 = all2 && qcn::epi_mode(L.ep[i]) == 2;
+  }
+  if (all1) em = 1;
+  else if (all2) em = 2;
+  else return QCN_ERR_UNSUPPORTED;
+  const float inv = 1.0f / in_scale;
+  static bool attr_done[4][QCN_MAX_DEV] = {};
+#define QCN_C16(EM_, KM_)                                                                          \
+  if (em == EM_ && (kmajor != 0) == KM_) {                                                         \
+    auto k = qcn::convnet_convs_kernel<EM_, KM_>;                                                  \
+    if (!qcn_set_lds_once((const void*)k, qcn::kConvnetLds, attr_done[(EM_ - 1) * 2 + KM_]))       \
+      return QCN_ERR_HIP;                                                                          \
+    hipLaunchKernelGGL(k, dim3(ncu), dim3(512), qcn::kConvnetLds, (hipStream_t)stream, x, nimg, inv, \
+                       L, a2, a4, a6);                                                             \
+    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;                                 \
+  }
+  QCN_C16(1, true) QCN_C16(1, false) QCN_C16(2, true) QCN_C16(2, false)
+#undef QCN_C16
+  return QCN_ERR_UNSUPPORTED;
 }
 
 int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_zp,

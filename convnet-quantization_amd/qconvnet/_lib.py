@@ -29,6 +29,13 @@ class QDQ(C.Structure):
     _fields_ = [("s1", C.c_float), ("z1", C.c_int32), ("inv2", C.c_float), ("z2", C.c_int32)]
 
 
+class ConvLayer(C.Structure):
+    """qcn_conv_layer_t"""
+    _fields_ = [("w", C.c_void_p), ("u", C.c_void_p), ("v", C.c_void_p), ("mult", C.c_void_p),
+                ("corr", C.c_void_p), ("x_zp", C.c_int32), ("y_zp", C.c_int32), ("relu", C.c_int32),
+                ("qdq", C.POINTER(QDQ))]
+
+
 vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_longlong
@@ -49,6 +56,7 @@ SIGNATURES = {
     "qcn_pack_conv1_weight": (i32, [vp, i32, vp, vp]),
     "qcn_conv3x3_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
                                     i32, C.POINTER(QDQ), vp, vp]),
+    "qcn_convnet_convs_f32_nchw": (i32, [vp, i32, f32, i32, C.POINTER(ConvLayer), vp, vp, vp, i32, vp]),
     "qcn_conv1_f32_nchw": (i32, [vp, i32, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,
                                  C.POINTER(QDQ), vp, vp, vp]),
     "qcn_conv12_fused_f32_nchw": (i32, [vp, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,

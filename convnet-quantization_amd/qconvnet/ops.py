@@ -181,6 +181,36 @@ def conv12_fused(x, in_scale, in_zp, l1, l2, out=None):
     return out
 
 
+def conv_layers(layers, in_zp):
+    """The six conv layers of SimpleConvNet (objects with w, u, v, mult, corr,
+    z_x, z_y, relu, qdq) as the qcn_conv_layer_t array convnet_convs() takes.
+    Built once per model: it holds the device pointers and the QDQ structs."""
+    arr = (_lib.ConvLayer * 6)()
+    for i, d in enumerate(layers):
+        arr[i] = _lib.ConvLayer(_ptr(d.w), _ptr(d.u), _ptr(d.v), _ptr(d.mult), _ptr(d.corr),
+                                int(in_zp) if i == 0 else int(d.z_x), int(d.z_y), int(bool(d.relu)),
+                                C.pointer(d.qdq) if d.qdq is not None else None)
+    return arr
+
+
+def convnet_convs(x, in_scale, in_zp, layers, a2, a4, a6, kmajor=True):
+    """QuantStub + conv1 .. conv6 in one persistent launch (conv6's pooled
+    output chunk-major into a6 [128, n, 32] when kmajor, else NHWC
+    [n, 4, 4, 256]).  ``layers``: conv_layers().
+    Returns False when the launch does not apply (fewer than 4 images per
+    CU, or mixed epilogue forms); the caller then runs the three launches."""
+    _need(x, torch.float32, "convnet_convs.x")
+    n = x.shape[0]
+    if tuple(x.shape[1:]) != (3, 32, 32):
+        raise ValueError("convnet_convs expects [n,3,32,32]")
+    rc = lib().qcn_convnet_convs_f32_nchw(_ptr(x), n, float(in_scale), int(in_zp), layers, _ptr(a2),
+                                          _ptr(a4), _ptr(a6), int(bool(kmajor)), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "convnet_convs")
+    return True
+
+
 def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=False, out=None,
               out_f=None):
     _need(x, torch.uint8, "linear.x")

@@ -218,6 +218,11 @@ class QuantizedConvNet:
         self.fuse12 = fuse12
         self.fuse_pairs = True   # conv3+conv4 / conv5+conv6 as one launch each
         self.fc_head = True      # fc1 -> fc2 as the split-K head (False: two linear launches)
+        # QuantStub + conv1 .. conv6 as one persistent launch where the library
+        # takes it (>= 4 images per CU; False: conv12 + the two pair launches)
+        self.fuse_convs = True
+        self._convs_ok = {}      # batch size -> whether the one-launch convs ran
+        self._conv_layers = None
         self._bufs = {}
         self._graphs = {}
         self._upload()
@@ -303,6 +308,8 @@ class QuantizedConvNet:
         """Names of the launches run() marks, in order (conv1+conv2 are one
         launch when fused, conv3+conv4 / conv5+conv6 one launch each when
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
+        if self._convs(x_shape, keep) and self._convs_ok.get(x_shape[0]):
+            return ("conv1_6", "fc12") if self._head(x_shape[0], keep) else ("conv1_6", "fc1", "fc2")
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
             names[names.index("conv3"):names.index("conv6") + 1] = ["conv34", "conv56"]
@@ -336,6 +343,11 @@ class QuantizedConvNet:
     def _fused(self, x_shape):
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
 
+    def _convs(self, x_shape, keep):
+        """The one-launch conv1 .. conv6 applies to this forward (the library
+        may still decline the batch size: _convs_ok records that per size)."""
+        return self.fuse_convs and self._fused(x_shape) and self._pairs(keep)
+
     def run(self, x, keep=False, marks=None, slot=0):
         """Launch the whole int8 forward on the current stream of the model's
         device (no sync).
@@ -363,7 +375,21 @@ class QuantizedConvNet:
         d = L[0]
         names = ["a2", "a3", "a4", "a5", "a6"]
         head = self._head(n, keep)
-        if self._fused(x.shape):
+        convs_done = False
+        if self._convs(x.shape, keep) and self._convs_ok.get(n, True):
+            if head and "a6k" not in b:
+                b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
+            if self._conv_layers is None:
+                self._conv_layers = ops.conv_layers(L, self.in_zp)
+            convs_done = ops.convnet_convs(x, self.in_scale, self.in_zp, self._conv_layers, b["a2"],
+                                           b["a4"], b["a6k"] if head else b["a6"], kmajor=head)
+            self._convs_ok[n] = convs_done
+            if convs_done:
+                mark()
+                prev, first = b["a6"], 6
+        if convs_done:
+            pass
+        elif self._fused(x.shape):
             ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
             mark()
             prev, first = b["a2"], 2

@@ -43,6 +43,22 @@ typedef struct qcn_qdq_t {
   int32_t z2;
 } qcn_qdq_t;
 
+/* One conv of SimpleConvNet for qcn_convnet_convs_f32_nchw: packed weights
+ * (qcn_pack_conv1_weight for conv1, qcn_pack_conv3x3_weight otherwise), the
+ * requant constants, the input / output zero points, ReLU and the optional
+ * QDQ hand-off into the next layer. */
+typedef struct qcn_conv_layer_t {
+  const int8_t* w;
+  const float* u;
+  const float* v;
+  const float* mult;
+  const int32_t* corr;
+  int32_t x_zp;
+  int32_t y_zp;
+  int32_t relu;
+  const qcn_qdq_t* qdq;
+} qcn_conv_layer_t;
+
 /* Library version (major*10000 + minor*100 + patch). */
 int qcn_version(void);
 
@@ -104,6 +120,20 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
  * (baseline_model.py:13, :60): fp32 NCHW [nimg,3,hw,hw] in, quantized with
  * (in_scale, in_zp), 3x3 conv to 64 channels, u8 NHWC out.  q_in (optional,
  * may be NULL) receives the quantized input, u8 NHWC. */
+/* A1 + conv1 .. conv6 of SimpleConvNet (baseline_model.py:60-72; per-layer
+ * QDQ form custom_quantization_model.py:233-255) in ONE persistent launch:
+ * fp32 NCHW [nimg,3,32,32] in (quantized with in_scale / in_zp ==
+ * layers[0].x_zp), conv6's pooled output into a6: chunk-major
+ * ([128][nimg][32], the classifier head's input) when kmajor != 0, NHWC
+ * [nimg,4,4,256] otherwise; a2 ([nimg,16,16,64]) and a4 ([nimg,8,8,128]) are
+ * written on the way.  Each workgroup carries its own
+ * images through all six convs, so the results are those of
+ * qcn_conv12_fused_f32_nchw + two qcn_conv3x3_pair_u8s8 launches bit for
+ * bit.  QCN_ERR_UNSUPPORTED when nimg < 4 x CUs or conv3..conv6 are not all
+ * on the same fast epilogue (the caller then launches the three kernels). */
+int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
+                               const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
+                               int kmajor, void* stream);
 int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_zp,
                        const int8_t* w1_packed, const float* u, const float* v, const float* mult,
                        const int32_t* corr, int y_zp, int relu, const qcn_qdq_t* qdq, uint8_t* y,

@@ -1,8 +1,9 @@
 """GPU parity at the BASELINE configs themselves (not at a reduced batch):
 
 * configs[2] — full static int8 at batch 1024: the DEFAULT launch sequence
-  bench.py times (conv12 -> conv34 -> conv56 with chunk-major output -> fused
-  classifier head) bit-exact to torch.ao eager static int8 (fbgemm) over the
+  bench.py times (since r04 conv1 .. conv6 in one persistent launch with
+  chunk-major output -> the classifier head; before, conv12 -> conv34 ->
+  conv56 -> head, still the path below 4 images per CU) bit-exact to torch.ao eager static int8 (fbgemm) over the
   same 1024 images (tests/golden/net_static_int8_b1024*.npz, written by
   oracle/make_golden.py's gen_net_headline): a2, a4, conv6's chunk-major
   output, fc1 by hash; u8 and fp32 logits in full;
@@ -20,7 +21,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-HEADLINE = ("conv12", "conv34", "conv56", "fc12")
+HEADLINE = ("conv1_6", "fc12")
+THREE = ("conv12", "conv34", "conv56", "fc12")   # fuse_convs=False / < 4 images per CU
 
 
 @pytest.fixture(scope="module")
@@ -69,9 +71,9 @@ def test_headline_launch_sequence_equals_torchao(dev, golden_dir, per_channel):
     x = torch_ref.synthetic_images(n, 0)
     assert netfix.sha(x) == str(z["x_sha"])
     xd = torch.from_numpy(x).to(dev)
-    assert model.kernel_names(xd.shape) == HEADLINE
     model.run(xd)
     torch.cuda.synchronize()
+    assert model.kernel_names(xd.shape) == HEADLINE
     _check_headline_bufs(model, n, z)
     # the HIP-graph replay of the same sequence
     model.capture_graph(xd.clone())
@@ -79,6 +81,35 @@ def test_headline_launch_sequence_equals_torchao(dev, golden_dir, per_channel):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), z["logits"])
     assert np.array_equal(model(torch.from_numpy(x)).argmax(1).numpy(), z["argmax"])
+
+
+@pytest.mark.parametrize("mode", ["static", "qdq"])
+@pytest.mark.parametrize("n", [1024, 1031, 1539, 2048])
+def test_one_launch_convs_equal_three_launches(dev, golden_dir, mode, n):
+    """conv1 .. conv6 in one persistent launch (qcn_convnet_convs_f32_nchw):
+    a2, a4, conv6's chunk-major output and the logits equal the three-launch
+    path (conv12 -> conv3+4 -> conv5+6) bit for bit, at exactly 4 images per
+    CU, ragged batches (some workgroups one image more, a last conv5+6 tile
+    with one image) and 8 per CU; static and per-layer QDQ (the one-fma
+    hand-off form) nets."""
+    import netfix
+    from oracle import torch_ref
+    from qconvnet.qmodel import QuantizedConvNet
+    z = netfix.load()
+    spec = netfix.static_spec(z)[0] if mode == "static" else netfix.qdq_spec(netfix.load())
+    one, three = QuantizedConvNet(spec, dev), QuantizedConvNet(spec, dev)
+    three.fuse_convs = False
+    x = torch.from_numpy(torch_ref.synthetic_images(n, 3)).to(dev)
+    l1 = one.run(x).clone()
+    l3 = three.run(x).clone()
+    torch.cuda.synchronize()
+    head = n % 128 == 0   # the split-K head's row tile; else fc1 / fc2 launches on NHWC a6
+    assert one.kernel_names(x.shape) == (HEADLINE if head else ("conv1_6", "fc1", "fc2"))
+    assert three.kernel_names(x.shape) == (THREE if head else THREE[:3] + ("fc1", "fc2"))
+    b1, b3 = one.buffers(n), three.buffers(n)
+    for k in ("a2", "a4", "a6k" if head else "a6", "f1"):
+        assert torch.equal(b1[k], b3[k]), k
+    assert torch.equal(l1, l3)
 
 
 def test_batch_8192_shards_equal_1024(dev, golden_dir):
@@ -89,9 +120,9 @@ def test_batch_8192_shards_equal_1024(dev, golden_dir):
     z = _fixture(golden_dir, "net_static_int8_b1024.npz")
     model = _headline_model(False, dev)
     x = torch.from_numpy(torch_ref.synthetic_images(8192, 0)).to(dev)
-    assert model.kernel_names(x.shape) == HEADLINE
     full = model.run(x).clone()
     torch.cuda.synchronize()
+    assert model.kernel_names(x.shape) == HEADLINE
     _check_headline_bufs(model, 8192, z, rows=slice(0, 1024))
     for r in range(8):
         part = model.run(x[r * 1024:(r + 1) * 1024].contiguous())

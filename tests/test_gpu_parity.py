@@ -476,6 +476,7 @@ def test_conv_pairs_qdq_equal_layerwise(dev, per_channel):
     spec = netfix.qdq_spec(z)
     x = torch.from_numpy(netfix.images(z)).to(dev)
     model = QuantizedConvNet(spec, dev)
+    model.fuse_convs = False
     assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     a4_p = model.buffers(x.shape[0])["a4"].clone()
@@ -500,6 +501,7 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
     x = torch.from_numpy(netfix.images(z)).to(dev)
     n = x.shape[0]
     model = QuantizedConvNet(spec, dev)
+    model.fuse_convs = False
     assert "conv34" in model.kernel_names(x.shape)
     out_p = model.run(x).clone()
     b = model.buffers(n)
@@ -534,6 +536,7 @@ def test_conv_pair_workgroup_shapes_equal_layerwise(dev, mode, n):
     spec = netfix.static_spec(netfix.load(False))[0] if mode == "static" else netfix.qdq_spec(netfix.load(False))
     x = torch.from_numpy(torch_ref.synthetic_images(n, 13)).to(dev)
     model = QuantizedConvNet(spec, dev)
+    model.fuse_convs = False   # the pair launches themselves (the one-launch convs: test_gpu_headline)
     assert model.kernel_names(x.shape)[1:3] == ("conv34", "conv56")
     out_p = model.run(x).clone()
     a4_p = model.buffers(n)["a4"].clone()
