@@ -1,7 +1,6 @@
 # A/B two configurations on the same box (boxes differ by up to ~12 %).  Each
 # argument is a string of env assignments, e.g.
 #   bash tools/ab.sh "QCN_LIB=tools/ab/libqconvnet_a.so" "" 3
-#   bash tools/ab.sh "QCN_FC_HEAD=linear" "" 3
 set -e
 A=$1; B=$2; N=${3:-3}
 for i in $(seq $N); do
