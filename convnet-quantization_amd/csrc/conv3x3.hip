@@ -106,7 +106,12 @@ struct ConvCfg {
                       : (PXB >= IMG ? (PXB % IMG == 0) : (H % R == 0)), "rows tile the image");
   static_assert(!POOL || (R % 2 == 0), "pooled rows come in pairs");
   static_assert(NG >= 1 && WBUF % 1024 == 0, "weight ring split");
-  static_assert(!POOL || JT == 4, "pooled tiles are the four quadrants");
+  // pooled tiles: the four 2x2 quadrants as four 32-pixel blocks (JT = 4), or
+  // one 8x8 image on 64-pixel tiles (JT = 2, "lane-pooled"): block j holds the
+  // column-parity-j quadrants, lanes 0-15 / 16-31 the two row parities of the
+  // 16 pooled pixels, and the row max is a v_permlane16_swap
+  static constexpr bool kLanePool = POOL && JT == 2;
+  static_assert(!POOL || JT == 4 || (HW == 8 && WPX == 1 && !RB_), "pooled tiles are the four quadrants");
   static_assert(JT == 2 || JT == 4, "64- or 128-pixel wave tiles");
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __device__ static constexpr int slot(int seg, int prow, int pcol) {
@@ -212,6 +217,11 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
       const int rg = 4 * g + e;
       a[e] = accs[0][rg];
       if constexpr (NQ == 4) a[e] = max(max(a[e], accs[1][rg]), max(accs[2][rg], accs[3][rg]));
+      if constexpr (NQ == 2) {   // lane-pooled tiles: column pair in registers, row pair across lanes l ^ 16
+        a[e] = max(a[e], accs[1][rg]);
+        const auto r = __builtin_amdgcn_permlane16_swap(a[e], a[e], false, false);
+        a[e] = max((int)r[0], (int)r[1]);
+      }
     }
     if constexpr (EM != 0) {
       // scalar fma / mul (built with -fno-slp-vectorize so they stay scalar):
@@ -336,7 +346,12 @@ struct PatchAddr {
         base[j] = (i + 2 * seg) * C::RS + (m % C::W) * C::PS + hi * 16;
         continue;
       }
-      if constexpr (C::kPool) {
+      if constexpr (C::kLanePool) {
+        const int q = l32 & 15, rp = l32 >> 4;   // pooled pixel (4 x 4), row parity
+        seg = 0;
+        prow = 2 * (q >> 2) + rp;
+        pcol = 2 * (q & 3) + j;
+      } else if constexpr (C::kPool) {
         constexpr int PW = C::W / 2, PR = C::R / 2;
         const int q = wp * 32 + l32;
         seg = q / (PR * PW);
@@ -538,7 +553,9 @@ QCN_DEV void conv_epilogue(v16i (&acc)[C::WI][C::JT], const ConvEpi& ep, uint8_t
   for (int i = 0; i < C::WI; ++i) {
     const int co_base = wc * 32 * C::WI + i * 32;
     const EpiK K = load_epik_lds(ek, COUT, co_base, hi);
-    if constexpr (POOL) {
+    if constexpr (C::kLanePool) {   // lanes l32 and l32 ^ 16 hold the same pooled pixel
+      epilogue_tile_kf<2>(acc[i], K, ep, co_base, hi, lout + (l32 & 15) * C::OS);
+    } else if constexpr (POOL) {
       const int opx = wp * 32 + l32;
       epilogue_tile_kf<4>(acc[i], K, ep, co_base, hi, lout + opx * C::OS);
     } else {
@@ -857,9 +874,9 @@ QCN_DEV void ga_prefetch(GaFrag<C, D>& g, const int8_t* __restrict__ wpk, int wa
 template <class C, int D, int CST = C::WBUF, class Bar = WgBar>
 QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ wpk,
                               const int* __restrict__ corr, int wave, int lane,
-                              v16i (&acc)[C::WI][4], GaFrag<C, D>& g, Bar&& bar = Bar{}, int co0 = 0) {
+                              v16i (&acc)[C::WI][C::JT], GaFrag<C, D>& g, Bar&& bar = Bar{}, int co0 = 0) {
   constexpr int CB = C::kCin / 64;
-  constexpr int WI = C::WI, MPS = C::MPS, S = 2 * C::NCH;
+  constexpr int WI = C::WI, JT = C::JT, MPS = C::MPS, S = 2 * C::NCH;
   static_assert(D >= 1 && D < S, "prefetch depth");
   const int wc = wave % C::WCO, wp = wave / C::WCO;
   const int l32 = lane & 31, hi = lane >> 5;
@@ -875,20 +892,20 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
     return *reinterpret_cast<const v4i*>(patch + pa.base[j] + PatchAddr<C>::delta(tap, j) + cb * 64 +
                                          kk * 32);
   };
-  v4i fb[2][4];
+  v4i fb[2][JT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) fb[0][j] = rd_b(0, j);
+  for (int j = 0; j < JT; ++j) fb[0][j] = rd_b(0, j);
 #pragma unroll
   for (int s = 0; s < S; ++s) {
 #pragma unroll
     for (int m = 0; m < MPS; ++m) {
-      // next step's four B fragments spread over the step's MFMAs (every
-      // other one when there are eight), the A loads of step s + D mid-step
-      constexpr int BSP = MPS / 4;
+      // next step's JT B fragments spread over the step's MFMAs (every
+      // other one when there are 2 JT), the A loads of step s + D mid-step
+      constexpr int BSP = MPS / JT;
       if (s + 1 < S && m % BSP == 0) fb[(s + 1) & 1][m / BSP] = rd_b(s + 1, m / BSP);
       __builtin_amdgcn_sched_barrier(0);
-      acc[m / 4][m % 4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
-          g.fa[s % (D + 1)][m / 4], fb[s & 1][m % 4], s == 0 ? c0[m / 4] : acc[m / 4][m % 4], 0, 0, 0);
+      acc[m / JT][m % JT] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+          g.fa[s % (D + 1)][m / JT], fb[s & 1][m % JT], s == 0 ? c0[m / JT] : acc[m / JT][m % JT], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + D < S && m == MPS / 2 - 1) {
         // slot (s + D) % (D + 1) == (s - 1) % (D + 1): consumed by step s - 1
@@ -900,7 +917,7 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
 #pragma unroll
       for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[i][j]));
+        for (int j = 0; j < JT; ++j) asm volatile("" : "+v"(acc[i][j]));
     }
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -913,7 +930,7 @@ QCN_DEV void conv_mainloop_ga(const uint8_t* patch, const int8_t* __restrict__ w
 template <class CA, class CB>
 struct PairGaCfg {
   static_assert(!CA::kPool && CA::kCout == CB::kCin, "A feeds B");
-  static_assert(CA::JT == 4 && CB::JT == 4, "128-pixel wave tiles (the GA loop)");
+  static_assert(CA::JT == CB::JT, "one wave-tile width for both convs (128 or 64 pixels)");
   // (B may own a slice of the couts with a narrower wave tile: the patch
   // layout depends only on B's input side)
   static_assert(CA::NT == CB::NT && CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CB::R &&
@@ -923,7 +940,7 @@ struct PairGaCfg {
   static constexpr int OFF_EA = PATCH;
   static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
   static constexpr int LDS = OFF_EB + 12 * CB::kCout;
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static_assert(LDS <= (CA::NT >= 512 ? 160 : 80) * 1024, "two 4-wave or one 8-wave workgroup per CU");
 };
 
 // One tile (CA::PXB pixels of whole images) through A then B, weights from
@@ -945,7 +962,7 @@ QCN_DEV void convpair_ga_tile(int tile, const uint8_t* __restrict__ x, int nimg,
   ga_prefetch<CA, D>(ga, wa, wave, lane);
   stage_patch<CA>(x, nimg, x_zp, n0, y0, lb, tid);
   bar();
-  v16i acc[CA::WI][4];
+  v16i acc[CA::WI][CA::JT];
   conv_mainloop_ga<CA, D>(lb, wa, epa.corr, wave, lane, acc, ga, bar);
   GaFrag<CB, D> gb;
   ga_prefetch<CB, D>(gb, wb, wave, lane);   // B's first loads ride under A's epilogue
@@ -974,7 +991,7 @@ QCN_DEV void convpair_ga_body(int tile, const uint8_t* __restrict__ x, int nimg,
 }
 
 template <class CA, class CB, int D>
-__global__ __launch_bounds__(CA::NT, 2)
+__global__ __launch_bounds__(CA::NT, CA::NT >= 512 ? 1 : 2)
 void convpair_ga_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
                         const int8_t* __restrict__ wa, ConvEpi epa, int xb_zp,
                         const int8_t* __restrict__ wb, ConvEpi epb, uint8_t* __restrict__ y) {
@@ -2092,6 +2109,12 @@ struct ConvnetLayers {
   int x_zp[6];   // input zero point of conv i (x_zp[0]: the QuantStub's)
 };
 
+// one image per workgroup (<= 1 image per CU): the 8-wave forms of the pairs
+using SmA3 = ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>;
+using SmB4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>;
+using SmA5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false, 1, 2>;
+using SmB6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true, 1, 2>;
+
 using WsA3 = ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>;
 using WsB4 = ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>;
 using WsA5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
@@ -2100,6 +2123,7 @@ using WsB6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE34_D>::LDS,
                                                    PairWs<WsA5, WsB6, QCN_PIPE34_D>::LDS));
+constexpr int kConvnetSmLds = cmax(Conv12P::LDS, cmax(PairCfg<SmA3, SmB4>::LDS, PairGaCfg<SmA5, SmB6>::LDS));
 
 QCN_DEV void phase_boundary() {
   // every wave's stores of the phase complete, all LDS use done, default priority
@@ -2121,6 +2145,22 @@ void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, C
   phase_boundary();
   convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, L.x_zp[4], L.w[4], L.ep[4],
                                                                    L.x_zp[5], L.w[5], L.ep[5], a6);
+}
+
+// The same at one image per workgroup (batch <= CUs, e.g. configs[1]'s 256):
+// conv12p over the workgroup's image, then the 8-wave conv3+4 and conv5+6
+// pair bodies of the small-batch launches on that image.  Epilogue forms and
+// conv6's layout (ep.kmajor) are runtime here.
+__global__ __launch_bounds__(512, 1)
+void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv, ConvnetLayers L,
+                             uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
+  const int b = (int)blockIdx.x;
+  conv12p_body(b, (int)gridDim.x, 2, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1],
+               a2);
+  phase_boundary();
+  convpair_body<SmA3, SmB4>(b, a2, nimg, L.x_zp[2], L.w[2], L.ep[2], L.x_zp[3], L.w[3], L.ep[3], a4);
+  phase_boundary();
+  convpair_ga_body<SmA5, SmB6, 4>(b, a4, nimg, L.x_zp[4], L.w[4], L.ep[4], L.x_zp[5], L.w[5], L.ep[5], a6);
 }
 
 // --------------------------------------------------------------------------
@@ -2489,8 +2529,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // 64-cout x 64-pixel wave tiles, conv4 as 32-cout x 128-pixel tiles — so
     // each SIMD holds two waves of the image's work instead of one
     if (nimg <= ncu)
-      return launch_pair<ConvCfg<64, 128, 16, false, 4, 16, 96, 0, false, 2, 2>,
-                         ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true, 1, 4>>(
+      return launch_pair<SmA3, SmB4>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     using A3 = WsA3;
     using B4 = WsB4;
@@ -2505,12 +2544,12 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // into registers 4 K-steps ahead (convpair_ga_kernel)
     using A1 = WsA5;
     using B1 = WsB6;
-    // at or below one image per CU, conv6's couts split over two workgroups
-    // (conv5 computed by both): twice the workgroups.  Batch 256: 22.3 ->
-    // 20.6-21.7 us; batch 512 (one workgroup per CU either way) 27.9 -> 33.3
-    // us, so only at <= 1 image per CU
+    // at or below one image per CU: one image per 8-wave workgroup (conv5 and
+    // conv6 as 32-cout x 64-pixel wave tiles, conv6 lane-pooled), two waves
+    // per SIMD and no recomputation (r03's form split conv6's couts over two
+    // 4-wave workgroups, each computing all of conv5: 4/3 of the MFMAs)
     if (nimg <= ncu)
-      return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
+      return launch_pair_ga<SmA5, SmB6, 4>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // two or more image pairs per CU: the persistent wave-specialised kernel
     if (QCN_WS56 && nimg >= 4 * ncu)
@@ -2614,6 +2653,15 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
   if ((long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
   const int ncu = qcn_cu_count();
   if (ncu <= 0) return QCN_ERR_HIP;
+  const float inv = 1.0f / in_scale;
+  if (nimg <= ncu) {   // one image per workgroup
+    static bool sm_done[QCN_MAX_DEV] = {};
+    if (!qcn_set_lds_once((const void*)qcn::convnet_convs_sm_kernel, qcn::kConvnetSmLds, sm_done))
+      return QCN_ERR_HIP;
+    hipLaunchKernelGGL(qcn::convnet_convs_sm_kernel, dim3(nimg), dim3(512), qcn::kConvnetSmLds,
+                       (hipStream_t)stream, x, nimg, inv, L, a2, a4, a6);
+    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+  }
   // the two pair phases are the wave-specialised kernels of >= 4 images per CU;
   // conv3..conv6 all on the FBGEMM fast epilogue or all on the one-fma QDQ form
   if (nimg < 4 * ncu) return QCN_ERR_UNSUPPORTED;
@@ -2626,7 +2674,6 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
   if (all1) em = 1;
   else if (all2) em = 2;
   else return QCN_ERR_UNSUPPORTED;
-  const float inv = 1.0f / in_scale;
   static bool attr_done[4][QCN_MAX_DEV] = {};
 #define QCN_C16(EM_, KM_)                                                                          \
   if (em == EM_ && (kmajor != 0) == KM_) {                                                         \

@@ -84,14 +84,15 @@ def test_headline_launch_sequence_equals_torchao(dev, golden_dir, per_channel):
 
 
 @pytest.mark.parametrize("mode", ["static", "qdq"])
-@pytest.mark.parametrize("n", [1024, 1031, 1539, 2048])
+@pytest.mark.parametrize("n", [6, 256, 1024, 1031, 1539, 2048])
 def test_one_launch_convs_equal_three_launches(dev, golden_dir, mode, n):
     """conv1 .. conv6 in one persistent launch (qcn_convnet_convs_f32_nchw):
-    a2, a4, conv6's chunk-major output and the logits equal the three-launch
-    path (conv12 -> conv3+4 -> conv5+6) bit for bit, at exactly 4 images per
-    CU, ragged batches (some workgroups one image more, a last conv5+6 tile
-    with one image) and 8 per CU; static and per-layer QDQ (the one-fma
-    hand-off form) nets."""
+    a2, a4, conv6's output and the logits equal the three-launch path
+    (conv12 -> conv3+4 -> conv5+6) bit for bit: one image per workgroup at
+    <= 1 image per CU (6, 256: the 8-wave small-batch phases), exactly 4
+    images per CU, ragged batches (some workgroups one image more, a last
+    conv5+6 tile with one image) and 8 per CU; static and per-layer QDQ (the
+    one-fma hand-off form) nets."""
     import netfix
     from oracle import torch_ref
     from qconvnet.qmodel import QuantizedConvNet
