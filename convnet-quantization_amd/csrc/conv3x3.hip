@@ -43,6 +43,11 @@
 #ifndef QCN_WS56
 #define QCN_WS56 1
 #endif
+// conv5+6 at <= 1 image per CU on one 8-wave workgroup per image (lane-pooled
+// conv6); 0 keeps r03's cout-split form (diagnostic builds)
+#ifndef QCN_SM56
+#define QCN_SM56 1
+#endif
 
 namespace qcn {
 
@@ -2125,6 +2130,27 @@ constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE3
                                                    PairWs<WsA5, WsB6, QCN_PIPE34_D>::LDS));
 constexpr int kConvnetSmLds = cmax(Conv12P::LDS, cmax(PairCfg<SmA3, SmB4>::LDS, PairGaCfg<SmA5, SmB6>::LDS));
 
+// Diagnostic builds only (tools/clock: -DQCN_CONVNET_STAMP): s_memtime /
+// s_memrealtime of wave 0 at the start, after each phase and at the end of
+// every workgroup, stored by one lane with plain vector stores.  The product
+// library compiles none of it.
+#ifdef QCN_CONVNET_STAMP
+__device__ unsigned long long g_c16_stamp[4096][8];
+QCN_DEV void c16_stamp(int i) {
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if ((threadIdx.x >> 6) == 0 && lane == 0 && blockIdx.x < 4096) {
+    volatile unsigned long long* d = g_c16_stamp[blockIdx.x];
+    d[i] = t + lane;
+    d[4 + i] = r + lane;
+  }
+}
+#define C16_STAMP(i) c16_stamp(i)
+#else
+#define C16_STAMP(i)
+#endif
+
 QCN_DEV void phase_boundary() {
   // every wave's stores of the phase complete, all LDS use done, default priority
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -2138,13 +2164,20 @@ void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, C
                           uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
   const int b = (int)blockIdx.x, G = (int)gridDim.x;
   const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
+  C16_STAMP(0);
   conv12p_body(b, G, T, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1], a2);
   phase_boundary();
+  C16_STAMP(1);
   convpair_ws_body<WsA3, WsB4, QCN_PIPE34_D, EM, EM, false>(b, G, a2, nimg, L.x_zp[2], L.w[2], L.ep[2],
                                                             L.x_zp[3], L.w[3], L.ep[3], a4);
   phase_boundary();
+  C16_STAMP(2);
   convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, L.x_zp[4], L.w[4], L.ep[4],
                                                                    L.x_zp[5], L.w[5], L.ep[5], a6);
+#ifdef QCN_CONVNET_STAMP
+  __syncthreads();
+#endif
+  C16_STAMP(3);
 }
 
 // The same at one image per workgroup (batch <= CUs, e.g. configs[1]'s 256):
@@ -2155,12 +2188,19 @@ __global__ __launch_bounds__(512, 1)
 void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv, ConvnetLayers L,
                              uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
   const int b = (int)blockIdx.x;
+  C16_STAMP(0);
   conv12p_body(b, (int)gridDim.x, 2, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1],
                a2);
   phase_boundary();
+  C16_STAMP(1);
   convpair_body<SmA3, SmB4>(b, a2, nimg, L.x_zp[2], L.w[2], L.ep[2], L.x_zp[3], L.w[3], L.ep[3], a4);
   phase_boundary();
+  C16_STAMP(2);
   convpair_ga_body<SmA5, SmB6, 4>(b, a4, nimg, L.x_zp[4], L.w[4], L.ep[4], L.x_zp[5], L.w[5], L.ep[5], a6);
+#ifdef QCN_CONVNET_STAMP
+  __syncthreads();
+#endif
+  C16_STAMP(3);
 }
 
 // --------------------------------------------------------------------------
@@ -2548,8 +2588,11 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // conv6 as 32-cout x 64-pixel wave tiles, conv6 lane-pooled), two waves
     // per SIMD and no recomputation (r03's form split conv6's couts over two
     // 4-wave workgroups, each computing all of conv5: 4/3 of the MFMAs)
-    if (nimg <= ncu)
+    if (QCN_SM56 && nimg <= ncu)
       return launch_pair_ga<SmA5, SmB6, 4>(
+          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    if (nimg <= ncu)
+      return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // two or more image pairs per CU: the persistent wave-specialised kernel
     if (QCN_WS56 && nimg >= 4 * ncu)

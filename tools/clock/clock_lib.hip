@@ -14,6 +14,8 @@
 // tools/clock_probe.py; the product library never contains a stamp.
 // the pipelined conv3+conv4 kernel's own stamps (g_p34_stamp) are compiled in
 #define QCN_PIPE34_STAMP 1
+// and the one-launch conv1..conv6 kernels' per-phase stamps (g_c16_stamp)
+#define QCN_CONVNET_STAMP 1
 #define qcn_conv3x3_pair_u8s8 qcn_conv3x3_pair_u8s8__product
 #define qcn_conv12_fused_f32_nchw qcn_conv12_fused_f32_nchw__product
 #include "conv3x3.hip"
@@ -203,8 +205,31 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+// The one-launch conv1..conv6's stamps of the last launch: [wg][t0..t3, r0..r3]
+// (start, after the conv12 phase, after the conv3+4 phase, end).
+int qcn_clock_read_c16(unsigned long long* host, int n) {
+  if (n <= 0 || n > 4096 || !host) return QCN_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_c16_stamp), (size_t)n * 64, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 // Copy kind's stamps of the last launch ([wg][t0, t1, r0, r1], n workgroups) to host.
+// kind 3: the one-launch conv1..conv6 (whole body).
 int qcn_clock_read(int kind, unsigned long long* host, int n) {
+  if (kind == 3) {
+    if (n <= 0 || n > 4096 || !host) return QCN_ERR_ARG;
+    static unsigned long long st[4096][8];
+    if (hipMemcpyFromSymbol(st, HIP_SYMBOL(qcn::g_c16_stamp), (size_t)n * 64, 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+      return QCN_ERR_HIP;
+    for (int w = 0; w < n; ++w) {
+      host[4 * w + 0] = st[w][0];
+      host[4 * w + 1] = st[w][3];
+      host[4 * w + 2] = st[w][4];
+      host[4 * w + 3] = st[w][7];
+    }
+    return QCN_OK;
+  }
   if (kind < 0 || kind > 2 || n <= 0 || n > qcn::kClkMaxWg || !host) return QCN_ERR_ARG;
   if ((kind == 1 && g_last34_ws) || (kind == 2 && g_last56_ws)) {
     // g_p34_stamp[k][wg] = [realtime start, memtime ..., realtime end]: the

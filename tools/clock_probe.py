@@ -33,11 +33,13 @@ import ctypes  # noqa: E402
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-KINDS = {"conv12": 0, "conv34": 1, "conv56": 2}
+KINDS = {"conv12": 0, "conv34": 1, "conv56": 2, "conv1_6": 3}
 MFMA_MAC_PER_CLK_SIMD = 1024   # v_mfma_i32_32x32x32_i8: 32768 MAC per 32 cycles
 
 
 def grid_of(name, n, ncu):
+    if name == "conv1_6":              # one launch: one image per workgroup, else persistent
+        return n if n <= ncu else ncu
     if name == "conv12":
         return min(n, ncu)
     if name == "conv34":               # persistent wave-specialised kernel from two images
@@ -64,6 +66,8 @@ def main():
     assert os.path.samefile(_lib.LIB_PATH, DIAG_LIB), "the diagnostic library must be the one loaded"
     fn = lib.qcn_clock_read
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    fn16 = lib.qcn_clock_read_c16
+    fn16.restype, fn16.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     mode = "qdq" if args.workload == "qdq" else "static"
@@ -118,6 +122,13 @@ def main():
                         "wg_mfma_cycles_per_simd": mfma_cyc_wg,
                         "launch_span_us": float((r1_.max() - r0_.min()) / 100.0),
                         "frac_at_2p4": frac, "mfma_issue_at_clock": frac * 2.4 / clock})
+            if n == "conv1_6":   # per-phase cycles of the one launch (median over workgroups)
+                b16 = np.zeros((g, 8), np.uint64)
+                _lib.check(fn16(b16.ctypes.data, g), "qcn_clock_read_c16")
+                t = b16[:, :4].astype(np.float64)
+                rec["phase_cycles_median"] = {
+                    ph: float(np.median(t[:, i + 1] - t[:, i]))
+                    for i, ph in enumerate(("conv12", "conv34", "conv56"))}
         out["kernels"][n] = rec
     print(json.dumps(out))
     for n, r in out["kernels"].items():
