@@ -43,10 +43,13 @@
 #ifndef QCN_WS56
 #define QCN_WS56 1
 #endif
-// conv5+6 at <= 1 image per CU on one 8-wave workgroup per image (lane-pooled
-// conv6); 0 keeps r03's cout-split form (diagnostic builds)
+// 1: the separate conv5+6 launch at <= 1 image per CU on one 8-wave workgroup
+// per image (lane-pooled conv6, the form the one-launch convs use there);
+// default 0 keeps r03's cout-split form, which is faster as a launch of its
+// own (batch 256: 54.8 vs 58.8 us per forward with three launches,
+// profiles/r04_diag_small_conv56_ab.txt) — diagnostic builds only
 #ifndef QCN_SM56
-#define QCN_SM56 1
+#define QCN_SM56 0
 #endif
 
 namespace qcn {
@@ -2108,6 +2111,17 @@ void conv12p_kernel(const float* __restrict__ x, int nimg, float in_inv, int in_
 // drained before the phase barrier; this CU never read those addresses
 // before in this launch, so its L1 holds no stale copy).  Same LDS, same
 // numerics, same code as the three launches (phase bodies shared).
+// the six layers as separate by-value kernel arguments (a struct of arrays
+// passed whole made the compiler copy it to scratch to take references into it)
+#define QCN_C16_PARAMS                                                                                   \
+  const int8_t* __restrict__ w0, ConvEpi e0, int z0, const int8_t* __restrict__ w1, ConvEpi e1, int z1, \
+      const int8_t* __restrict__ w2, ConvEpi e2, int z2, const int8_t* __restrict__ w3, ConvEpi e3,      \
+      int z3, const int8_t* __restrict__ w4, ConvEpi e4, int z4, const int8_t* __restrict__ w5,          \
+      ConvEpi e5, int z5
+#define QCN_C16_ARGS(L)                                                                                  \
+  (L).w[0], (L).ep[0], (L).x_zp[0], (L).w[1], (L).ep[1], (L).x_zp[1], (L).w[2], (L).ep[2], (L).x_zp[2],   \
+      (L).w[3], (L).ep[3], (L).x_zp[3], (L).w[4], (L).ep[4], (L).x_zp[4], (L).w[5], (L).ep[5], (L).x_zp[5]
+
 struct ConvnetLayers {
   const int8_t* w[6];
   ConvEpi ep[6];
@@ -2160,20 +2174,18 @@ QCN_DEV void phase_boundary() {
 
 template <int EM, bool KMAJOR>
 __global__ __launch_bounds__(512, 1)
-void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, ConvnetLayers L,
+void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, QCN_C16_PARAMS,
                           uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
   const int b = (int)blockIdx.x, G = (int)gridDim.x;
   const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
   C16_STAMP(0);
-  conv12p_body(b, G, T, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1], a2);
+  conv12p_body(b, G, T, x, nimg, in_inv, z0, w0, e0, z1, w1, e1, a2);
   phase_boundary();
   C16_STAMP(1);
-  convpair_ws_body<WsA3, WsB4, QCN_PIPE34_D, EM, EM, false>(b, G, a2, nimg, L.x_zp[2], L.w[2], L.ep[2],
-                                                            L.x_zp[3], L.w[3], L.ep[3], a4);
+  convpair_ws_body<WsA3, WsB4, QCN_PIPE34_D, EM, EM, false>(b, G, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
   phase_boundary();
   C16_STAMP(2);
-  convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, L.x_zp[4], L.w[4], L.ep[4],
-                                                                   L.x_zp[5], L.w[5], L.ep[5], a6);
+  convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif
@@ -2185,18 +2197,17 @@ void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, C
 // pair bodies of the small-batch launches on that image.  Epilogue forms and
 // conv6's layout (ep.kmajor) are runtime here.
 __global__ __launch_bounds__(512, 1)
-void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv, ConvnetLayers L,
+void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv, QCN_C16_PARAMS,
                              uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
   const int b = (int)blockIdx.x;
   C16_STAMP(0);
-  conv12p_body(b, (int)gridDim.x, 2, x, nimg, in_inv, L.x_zp[0], L.w[0], L.ep[0], L.x_zp[1], L.w[1], L.ep[1],
-               a2);
+  conv12p_body(b, (int)gridDim.x, 2, x, nimg, in_inv, z0, w0, e0, z1, w1, e1, a2);
   phase_boundary();
   C16_STAMP(1);
-  convpair_body<SmA3, SmB4>(b, a2, nimg, L.x_zp[2], L.w[2], L.ep[2], L.x_zp[3], L.w[3], L.ep[3], a4);
+  convpair_body<SmA3, SmB4>(b, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
   phase_boundary();
   C16_STAMP(2);
-  convpair_ga_body<SmA5, SmB6, 4>(b, a4, nimg, L.x_zp[4], L.w[4], L.ep[4], L.x_zp[5], L.w[5], L.ep[5], a6);
+  convpair_ga_body<SmA5, SmB6, 4>(b, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif
@@ -2584,13 +2595,16 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // into registers 4 K-steps ahead (convpair_ga_kernel)
     using A1 = WsA5;
     using B1 = WsB6;
-    // at or below one image per CU: one image per 8-wave workgroup (conv5 and
-    // conv6 as 32-cout x 64-pixel wave tiles, conv6 lane-pooled), two waves
-    // per SIMD and no recomputation (r03's form split conv6's couts over two
-    // 4-wave workgroups, each computing all of conv5: 4/3 of the MFMAs)
+    // at or below one image per CU (QCN_SM56): one image per 8-wave workgroup
+    // (conv5 and conv6 as 32-cout x 64-pixel wave tiles, conv6 lane-pooled) —
+    // no recomputation, but every workgroup streams all 885 KB of conv5+6
+    // weights from L2 for one image
     if (QCN_SM56 && nimg <= ncu)
       return launch_pair_ga<SmA5, SmB6, 4>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
+    // default: conv6's couts split over two 4-wave workgroups per image pair,
+    // each computing all of conv5 (4/3 of the MFMAs, half the weight bytes per
+    // image)
     if (nimg <= ncu)
       return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
@@ -2702,7 +2716,7 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
     if (!qcn_set_lds_once((const void*)qcn::convnet_convs_sm_kernel, qcn::kConvnetSmLds, sm_done))
       return QCN_ERR_HIP;
     hipLaunchKernelGGL(qcn::convnet_convs_sm_kernel, dim3(nimg), dim3(512), qcn::kConvnetSmLds,
-                       (hipStream_t)stream, x, nimg, inv, L, a2, a4, a6);
+                       (hipStream_t)stream, x, nimg, inv, QCN_C16_ARGS(L), a2, a4, a6);
     return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
   }
   // the two pair phases are the wave-specialised kernels of >= 4 images per CU;
@@ -2724,7 +2738,7 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
     if (!qcn_set_lds_once((const void*)k, qcn::kConvnetLds, attr_done[(EM_ - 1) * 2 + KM_]))       \
       return QCN_ERR_HIP;                                                                          \
     hipLaunchKernelGGL(k, dim3(ncu), dim3(512), qcn::kConvnetLds, (hipStream_t)stream, x, nimg, inv, \
-                       L, a2, a4, a6);                                                             \
+                       QCN_C16_ARGS(L), a2, a4, a6);                                               \
     return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;                                 \
   }
   QCN_C16(1, true) QCN_C16(1, false) QCN_C16(2, true) QCN_C16(2, false)

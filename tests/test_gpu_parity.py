@@ -523,8 +523,10 @@ def test_conv_pairs_equal_layerwise(dev, per_channel):
                          [("qdq", n) for n in (6, 256, 512, 1024, 1031)])
 def test_conv_pair_workgroup_shapes_equal_layerwise(dev, mode, n):
     """conv3+conv4 and conv5+conv6 at batch sizes around their tilings (256
-    CUs): at or below one image per CU conv3+4 and conv5+6 run one image on
-    8 waves (conv6 on lane-pooled 64-pixel tiles);
+    CUs): at or below one image per CU conv3+4 runs one image on 8 waves and
+    conv5+6 splits its output channels over two workgroups per image pair
+    (the one-launch convs' 8-wave conv5+6 with lane-pooled conv6:
+    test_gpu_headline::test_one_launch_convs_equal_three_launches);
     above, conv3+4 runs one image per 4-wave workgroup and conv5+6 two images
     per 4-wave workgroup; from two images per CU conv3+4, and from four conv5+6,
     run the persistent wave-specialised kernel (the last tile of conv5+6 holds

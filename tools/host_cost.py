@@ -18,6 +18,7 @@ folded = fold_state_dict(fp.state_dict())
 ranges = calibrate(folded, [torch.from_numpy(torch_ref.synthetic_images(64, 1))], "cpu")
 for mode, B in (("static", 128), ("static", 256), ("qdq", 256), ("static", 1024)):
     model = QuantizedConvNet(build_qspec(folded, ranges, mode), dev)
+    model.fuse_convs = "--three" not in sys.argv   # --three: conv12 / conv3+4 / conv5+6 launches
     x = torch.from_numpy(torch_ref.synthetic_images(B, 0)).to(dev)
     for _ in range(20):
         model.run(x)
