@@ -51,6 +51,10 @@
 #ifndef QCN_SM56
 #define QCN_SM56 0
 #endif
+// weight-prefetch depth (K-steps) of the one-image conv5+6 (build-time)
+#ifndef QCN_SM56_D
+#define QCN_SM56_D 4
+#endif
 
 namespace qcn {
 
@@ -2207,7 +2211,7 @@ void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv
   convpair_body<SmA3, SmB4>(b, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
   phase_boundary();
   C16_STAMP(2);
-  convpair_ga_body<SmA5, SmB6, 4>(b, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
+  convpair_ga_body<SmA5, SmB6, QCN_SM56_D>(b, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif
@@ -2600,7 +2604,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // no recomputation, but every workgroup streams all 885 KB of conv5+6
     // weights from L2 for one image
     if (QCN_SM56 && nimg <= ncu)
-      return launch_pair_ga<SmA5, SmB6, 4>(
+      return launch_pair_ga<SmA5, SmB6, QCN_SM56_D>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // default: conv6's couts split over two 4-wave workgroups per image pair,
     // each computing all of conv5 (4/3 of the MFMAs, half the weight bytes per
