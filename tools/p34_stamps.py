@@ -4,7 +4,11 @@ then the last launch's per-workgroup s_memtime stamps around every pipeline
 barrier; prints the median cycles of every interval over the workgroups and
 the in-kernel clock (MI355X_MICROARCH 'DVFS give-back' item 6).
 
-    QCN_LIB=.../libqconvnet_stamp.so python tools/p34_stamps.py [B]
+    QCN_LIB=.../libqconvnet_stamp.so python tools/p34_stamps.py [B] [KIND]
+
+KIND 0 / 1: the conv3+conv4 / conv5+conv6 pair launch; 2: the model's default
+forward (the one-launch conv1..conv6 under tools/clock's library), printing the
+stamps of both pair phases inside it.
 """
 import ctypes as C
 import os
@@ -45,12 +49,22 @@ def main():
         for _ in range(100):
             if kind == 0:
                 ops.conv_pair(a2, L[2], L[3], out)
-            else:
+            elif kind == 1:
                 ops.conv_pair(a4, L[4], L[5], out6, kmajor=True)
+            else:
+                model.run(x)
         torch.cuda.synchronize()
         n += 100
     lib = _lib.load()
     nwg = min(B, 256)
+    for k in ((kind,) if kind < 2 else (0, 1)):
+        if kind == 2:
+            print(f"## phase {'conv3+4' if k == 0 else 'conv5+6'} of the one-launch convs "
+                  f"({model.kernel_names(x.shape)})")
+        report(lib, k, nwg, n)
+
+
+def report(lib, kind, nwg, n):
     buf = np.zeros((1024, 64), np.uint64)
     rc = lib.qcn_diag_p34_stamps(C.c_int(kind), buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), C.c_int(1024))
     assert rc == 0, rc
