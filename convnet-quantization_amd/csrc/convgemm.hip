@@ -21,7 +21,14 @@
 #include "common.hpp"
 #include "qconvnet_abi.hpp"
 
+#include <algorithm>
+#include <cmath>
 #include <type_traits>
+
+// 0: the streaming joins keep the op sequence (diagnostic builds, A/B)
+#ifndef QCN_JOIN_AFF
+#define QCN_JOIN_AFF 1
+#endif
 
 namespace qcn {
 
@@ -554,7 +561,7 @@ constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t) {
   return pos - 1 - last;
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL, bool S2 = false>
+template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false>
 __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_kernel(GemmArgs a) {
   static_assert(!S2 || BL, "stride 2 reads its rows through the LDS ring");
   constexpr int KC = K / 32;
@@ -599,6 +606,8 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   const v2f s3v = {a.s3, a.s3};
   const v2f zr = {(float)a.z_r, (float)a.z_r}, sr = {a.s_r, a.s_r}, io = {a.inv_o, a.inv_o};
   const float zof = (float)a.z_o;
+  // ZO == 2: the join's one-form constants (ja, jb, jc) travel in s3, s_r, inv_o
+  const v2f jav = {a.s3, a.s3}, jbv = {a.s_r, a.s_r}, jcv = {a.inv_o, a.inv_o};
   const int lastp = (int)(a.npix - 1);   // npix < 2^31 - 256 (checked at the ABI)
 
   // 32-bit buffer offsets (activations, identity and output are < 2 GiB:
@@ -749,11 +758,15 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
         for (int e = 0; e < 4; e += 2) {
           const v2f yf = {(float)((w[g] >> (8 * e)) & 0xff), (float)((w[g] >> (8 * e + 8)) & 0xff)};
           const v2f rf = {(float)((rw >> (8 * e)) & 0xff), (float)((rw >> (8 * e + 8)) & 0xff)};
-          const v2f sm = ((yf - zpv) * s3v + (rf - zr) * sr) * io;
-          if constexpr (ZO) {
+          if constexpr (ZO != 0) {
+            // ZO == 2: the one-form join, 2 packed fma per 2 outputs instead of 6 packed ops
+            v2f sm;
+            if constexpr (ZO == 2) sm = __builtin_elementwise_fma(yf, jav, __builtin_elementwise_fma(rf, jbv, jcv));
+            else sm = ((yf - zpv) * s3v + (rf - zr) * sr) * io;
             o = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, e, o);
             o = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, e + 1, o);
-          } else {   // relu(s) * inv == max(s * inv, 0) since inv > 0
+          } else {
+            const v2f sm = ((yf - zpv) * s3v + (rf - zr) * sr) * io;   // relu(s) * inv == max(s * inv, 0) since inv > 0
             o = __builtin_amdgcn_cvt_pk_u8_f32(
                 __builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaxf(sm.x, 0.0f)) + zof, 0.0f, 255.0f), e, o);
             o = __builtin_amdgcn_cvt_pk_u8_f32(
@@ -790,7 +803,7 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   }
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, bool ZO, bool BL, bool S2 = false>
+template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false>
 int launch_stream(GemmArgs& a, hipStream_t st) {
   const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL, S2>;
   static int occ_dev[QCN_MAX_DEV] = {};
@@ -813,6 +826,74 @@ int launch_stream(GemmArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+// ---- host: the residual join in one form (the streaming kernel's ZO == 2)
+//
+// With ZO (output zero point 0: ReLU = saturation at 0) the streaming
+// kernel's join is out = sat(rne(((y - z3) s3 + (r - zr) sr) * inv_o)) over the
+// byte pair (y3, identity), in that fp32 op order.  It is replaced by
+// sat(rne(fma(y, ja, fma(r, jb, jc)))) when candidate constants near
+// (s3 inv_o, sr inv_o, -(z3 s3 + zr sr) inv_o) reproduce it for all 65536
+// pairs (an interval for jc per (ja, jb) candidate, then an exact fp32 check);
+// otherwise the kernel keeps the op sequence.  Cached per qparam set.
+namespace {
+
+float join_ref_host(int y, int r, float z3f, float s3, float zrf, float sr, float io) {
+  const float t1 = ((float)y - z3f) * s3;
+  const float t2 = ((float)r - zrf) * sr;
+  const float sm = (t1 + t2) * io;
+  return std::fmin(std::fmax(std::nearbyint(sm), 0.0f), 255.0f);
+}
+
+bool join_affine_solve(const GemmArgs& a, float* j) {
+  struct Entry { float s3, sr, io; int z3, zr; bool ok; float ja, jb, jc; };
+  static thread_local Entry cache[32];
+  static thread_local int ncache = 0, next = 0;
+  for (int i = 0; i < ncache; ++i) {
+    const Entry& e = cache[i];
+    if (e.s3 == a.s3 && e.sr == a.s_r && e.io == a.inv_o && e.z3 == a.zp_y && e.zr == a.z_r) {
+      j[0] = e.ja; j[1] = e.jb; j[2] = e.jc;
+      return e.ok;
+    }
+  }
+  const float z3f = (float)a.zp_y, zrf = (float)a.z_r;
+  static thread_local float ref[256 * 256];
+  for (int y = 0; y < 256; ++y)
+    for (int r = 0; r < 256; ++r) ref[y * 256 + r] = join_ref_host(y, r, z3f, a.s3, zrf, a.s_r, a.inv_o);
+  const double A0 = (double)a.s3 * a.inv_o, B0 = (double)a.s_r * a.inv_o;
+  const float fa0 = (float)A0, fb0 = (float)B0;
+  bool ok = false;
+  float ja = 0.f, jb = 0.f, jc = 0.f;
+  for (int k = 0; k < 25 && !ok; ++k) {   // ja, jb within +-2 ulp of the products
+    const float A = std::nextafter(fa0, (k % 5) < 2 ? 0.f : 1e9f), B = std::nextafter(fb0, (k / 5) < 2 ? 0.f : 1e9f);
+    const float Ac = (k % 5) == 2 ? fa0 : ((k % 5) == 4 ? std::nextafter(A, 1e9f) : ((k % 5) == 0 ? A : std::nextafter(A, 0.f)));
+    const float Bc = (k / 5) == 2 ? fb0 : ((k / 5) == 4 ? std::nextafter(B, 1e9f) : ((k / 5) == 0 ? B : std::nextafter(B, 0.f)));
+    if (!(Ac > 0.f) || !(Bc > 0.f)) continue;
+    double lb = -1e30, ub = 1e30;
+    for (int y = 0; y < 256; ++y)
+      for (int r = 0; r < 256; ++r) {
+        const double g = ref[y * 256 + r], base = (double)y * Ac + (double)r * Bc;
+        if (g > 0.0) lb = std::max(lb, g - 0.5 - base);
+        if (g < 255.0) ub = std::min(ub, g + 0.5 - base);
+      }
+    if (!(lb < ub)) continue;
+    const float C = (float)(lb > -1e29 && ub < 1e29 ? 0.5 * (lb + ub) : (lb > -1e29 ? lb + 0.25 : ub - 0.25));
+    bool exact = true;
+    for (int y = 0; y < 256 && exact; ++y)
+      for (int r = 0; r < 256; ++r) {
+        const float v = std::fma((float)y, Ac, std::fma((float)r, Bc, C));
+        if (std::fmin(std::fmax(std::nearbyint(v), 0.0f), 255.0f) != ref[y * 256 + r]) { exact = false; break; }
+      }
+    if (exact) { ok = true; ja = Ac; jb = Bc; jc = C; }
+  }
+  j[0] = ja; j[1] = jb; j[2] = jc;
+  cache[next] = Entry{a.s3, a.s_r, a.inv_o, a.zp_y, a.z_r, ok, ja, jb, jc};
+  next = (next + 1) % 32;
+  if (ncache < 32) ++ncache;
+  return ok;
+}
+
+}  // namespace
+
 template <int K, int NW, bool RESID, int P, bool BL, bool S2 = false>
 int stream_modes(GemmArgs& a, hipStream_t st) {
   if constexpr (S2) {   // the downsample conv: no ReLU, no join
@@ -820,10 +901,19 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
     return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true, true, true>(a, st)
                        : launch_stream<K, NW, false, P, 1, true, true, true>(a, st);
   } else if constexpr (RESID) {   // the join's conv has no ReLU (lo == 0)
-    const bool zo = a.z_o == 0;
+    // ZO: 0 general output zero point, 1 zero (ReLU = saturation), 2 zero with
+    // the join in its exact one form (join_affine_solve), whose constants
+    // replace s3 / s_r / inv_o in this launch's copy of the arguments
+    float j[3];
+    if (QCN_JOIN_AFF && a.z_o == 0 && join_affine_solve(a, j)) {
+      GemmArgs b = a;
+      b.s3 = j[0]; b.s_r = j[1]; b.inv_o = j[2];
+      return a.zp_y == 0 ? launch_stream<K, NW, true, P, 0, 2, BL>(b, st) : launch_stream<K, NW, true, P, 1, 2, BL>(b, st);
+    }
+    const int zo = a.z_o == 0 ? 1 : 0;
     if (a.zp_y == 0)
-      return zo ? launch_stream<K, NW, true, P, 0, true, BL>(a, st) : launch_stream<K, NW, true, P, 0, false, BL>(a, st);
-    return zo ? launch_stream<K, NW, true, P, 1, true, BL>(a, st) : launch_stream<K, NW, true, P, 1, false, BL>(a, st);
+      return zo ? launch_stream<K, NW, true, P, 0, 1, BL>(a, st) : launch_stream<K, NW, true, P, 0, 0, BL>(a, st);
+    return zo ? launch_stream<K, NW, true, P, 1, 1, BL>(a, st) : launch_stream<K, NW, true, P, 1, 0, BL>(a, st);
   } else {
     if (a.lo == 0) return a.zp_y == 0 ? launch_stream<K, NW, false, P, 0, true, BL>(a, st)
                                       : launch_stream<K, NW, false, P, 1, true, BL>(a, st);
@@ -1066,6 +1156,15 @@ int dispatch_stream(GemmArgs& a, hipStream_t st) {
 }
 
 }  // namespace qcn
+
+extern "C" int qcn_join_affine(float y_scale, int y_zp, float r_scale, int r_zp, float out_scale, float* out) {
+  if (!out || !(y_scale > 0.f) || !(r_scale > 0.f) || !(out_scale > 0.f) || y_zp < 0 || y_zp > 255 ||
+      r_zp < 0 || r_zp > 255)
+    return QCN_ERR_ARG;
+  qcn::GemmArgs a{};
+  a.s3 = y_scale; a.zp_y = y_zp; a.s_r = r_scale; a.z_r = r_zp; a.inv_o = 1.0f / out_scale;
+  return qcn::join_affine_solve(a, out) ? 1 : 0;
+}
 
 extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
                                        const int8_t* w_packed, int cout, int kh, int kw,

@@ -66,6 +66,7 @@ SIGNATURES = {
     "qcn_classifier_workspace_size": (i64, [i32, i32]),
     "qcn_pack_fc_kmajor": (i32, [vp, i32, i32, vp]),
     "qcn_qdq_affine": (i32, [C.POINTER(QDQ), i32, i32, vp]),
+    "qcn_join_affine": (i32, [f32, i32, f32, i32, f32, vp]),
     "qcn_conv3x3_pair_u8s8": (i32, [vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, i32,
                                     C.POINTER(QDQ), vp, i32, vp, vp, vp, vp, i32, i32,
                                     C.POINTER(QDQ), i32, vp, vp]),

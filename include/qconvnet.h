@@ -211,6 +211,15 @@ int qcn_pack_fc_kmajor(const int8_t* w, int n, int k, int8_t* out);
  * general requant + qdq sequence).  The conv launchers apply it themselves;
  * exported for the host tests (no device work). */
 int qcn_qdq_affine(const qcn_qdq_t* q, int y_zp, int lo, float* out);
+/* Host: the fused residual join of the ResNet bottleneck (out zero point 0,
+ * custom_quantization_model.py:94-101) in its one form: on success (returns
+ * 1) out[3] = {a, b, c} with
+ *   sat(rne(((y - y_zp) y_scale + (r - r_zp) r_scale) * fp32(1/out_scale)))
+ *     == sat(rne(fma(y, a, fma(r, b, c))))
+ * for all 256 x 256 byte pairs (y, r) in the kernel's fp32 op order; 0 when
+ * no exact form was found (the streaming kernel then keeps the sequence).
+ * Applied by qcn_conv_gemm_u8s8_nhwc itself; exported for the host tests. */
+int qcn_join_affine(float y_scale, int y_zp, float r_scale, int r_zp, float out_scale, float* out);
 int qcn_classifier_u8s8(const uint8_t* x, int m, int k, const int8_t* w1, int n1, const float* u1,
                         const float* v1, const float* mult1, const int32_t* corr1, int y1_zp,
                         int relu1, const int8_t* w2, int n2, const float* u2, const float* v2,

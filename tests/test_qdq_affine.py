@@ -99,3 +99,40 @@ def test_qdq_affine_exact_ties(lib):
                 form = _form(lib, F32(s1), z1, F32(s2), z2, z1, 0)
                 if form is not None:
                     _check(form, F32(s1), z1, F32(s2), z2, z1, 0)
+
+
+def _join_ref(y, r, s3, z3, sr, zr, so):
+    """The streaming kernel's fused join (out zero point 0) in its fp32 op
+    order: sat(rne(((y - z3) s3 + (r - zr) sr) * fp32(1/so)))."""
+    inv = F32(1) / F32(so)
+    sm = ((y - F32(z3)) * F32(s3) + (r - F32(zr)) * F32(sr)).astype(F32)
+    return np.clip(np.rint((sm * inv).astype(F32)), 0, 255)
+
+
+def test_join_affine_is_exact_on_every_byte_pair(lib):
+    """qcn_join_affine (the ResNet join's one form in conv1x1_stream_kernel):
+    whenever a form is returned, rne(fma(y, a, fma(r, b, c))) equals the
+    kernel's join on all 65536 (y3, identity) pairs; found for most layers."""
+    y = np.arange(256, dtype=F32)[:, None]
+    r = np.arange(256, dtype=F32)[None, :]
+    rng = np.random.default_rng(11)
+    found = 0
+    n = 40
+    for _ in range(n):
+        s3 = F32(10 ** rng.uniform(-2.5, -1))
+        sr = F32(s3 * 2 ** rng.uniform(-1.5, 1.5))
+        so = F32(max(s3, sr) * 2 ** rng.uniform(0, 1.5))
+        z3, zr = int(rng.integers(40, 220)), int(rng.integers(0, 8))
+        out = (C.c_float * 3)()
+        rc = lib.qcn_join_affine(C.c_float(s3), z3, C.c_float(sr), zr, C.c_float(so), out)
+        assert rc in (0, 1)
+        if rc == 0:
+            continue
+        found += 1
+        a, b, c = (np.float64(out[i]) for i in range(3))
+        inner = (r.astype(np.float64) * b + c).astype(F32)   # fma(r, b, c), one rounding
+        v = (y.astype(np.float64) * a + inner.astype(np.float64)).astype(F32)
+        got = np.clip(np.rint(v), 0, 255)
+        want = _join_ref(y, r, s3, z3, sr, zr, so)
+        assert np.array_equal(got, want), (s3, z3, sr, zr, so)
+    assert found >= 0.75 * n, found

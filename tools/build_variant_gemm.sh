@@ -1,0 +1,10 @@
+# Build a diagnostic variant of libqconvnet.so with convgemm.hip compiled with
+# extra defines (never the product library):
+#   bash tools/build_variant_gemm.sh NAME "-DQCN_JOIN_AFF=0"
+set -e
+cd "$(dirname "$0")/../convnet-quantization_amd/csrc"
+mkdir -p build/var_$1
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize \
+  -Wall -Wno-unused-function -I../../include -I. $2 -c convgemm.hip -o build/var_$1/convgemm.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../qconvnet/libqconvnet_$1.so build/conv3x3.o \
+  build/elementwise.o build/linear.o build/classifier.o build/convgen.o build/var_$1/convgemm.o build/resnet_qdq.o build/resnet_stem.o
