@@ -134,7 +134,7 @@ def load_payload(path):
 WARMUP_MIN_S = 0.1   # untimed forwards after the W warmup steps, at least this long
 
 
-def ramp_warmup(step, drain, warmup, world, dev, min_s=WARMUP_MIN_S):
+def ramp_warmup(step, drain, warmup, world, dev, min_s=WARMUP_MIN_S, sync=None):
     """The W warmup steps, then more untimed steps until at least min_s of
     back-to-back forwards have run.  After an idle spell the chip needs a few
     ms of load to reach the throughput it then holds: on one box the headline
@@ -142,16 +142,18 @@ def ramp_warmup(step, drain, warmup, world, dev, min_s=WARMUP_MIN_S):
     over 300-1000 timed steps), profiles/r03_diag_warmup.txt.  The extra step
     count comes from a 5-step probe and is the max over ranks, so every rank
     runs the same number of steps (their logits all-gathers pair up).
-    Returns the number of warmup steps run."""
+    Returns the number of warmup steps run.  ``sync`` waits for the device
+    (default torch.cuda.synchronize)."""
+    sync = sync or torch.cuda.synchronize
     for _ in range(warmup):
         step()
     drain()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(5):
         step()
     drain()
-    torch.cuda.synchronize()
+    sync()
     per = (time.perf_counter() - t0) / 5
     extra = max(0, int(np.ceil(min_s / max(per, 1e-6))) - warmup - 5)
     if world > 1:
@@ -162,7 +164,7 @@ def ramp_warmup(step, drain, warmup, world, dev, min_s=WARMUP_MIN_S):
     for _ in range(extra):
         step()
     drain()
-    torch.cuda.synchronize()
+    sync()
     return warmup + 5 + extra
 
 
@@ -355,21 +357,25 @@ PMC_PASSES = (("fetch", ("FETCH_SIZE",), None),
               ("write", ("WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"), None))
 
 
-def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static"):
+def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static", extra=(), totals=False):
     """One rocprofv3 --pmc pass over `bench.py --no-cpu --no-pmc` as a child
     process (never an exec).  Returns ({kernel: {counter: mean per dispatch}},
-    the child's JSON line) or raises."""
+    the child's JSON line) or raises; with totals, {kernel: {counter: [sum
+    over dispatches, dispatches]}} instead of the means."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         raise RuntimeError("rocprofv3 not on PATH")
     out = tempfile.mkdtemp(prefix="qcn_pmc_", dir="/tmp")
     cmd = [exe, "--pmc", *counters, "--kernel-include-regex", "qcn::", "-f", "csv", "-d", out,
            "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup",
-           "1", "--warmup-min-ms", "0", "--no-cpu", "--no-pmc", "--batch", str(batch), "--spec-file", spec_file]
+           "1", "--warmup-min-ms", "0", "--no-cpu", "--no-pmc", "--no-extra", "--batch", str(batch)]
+    if spec_file:
+        cmd += ["--spec-file", spec_file]
     if per_channel:
         cmd.append("--per-channel")
-    if mode != "static":
+    if mode == "qdq":
         cmd += ["--workload", "qdq"]
+    cmd += list(extra)
     env = dict(os.environ, TMPDIR="/tmp")
     p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                          text=True, start_new_session=True)
@@ -392,6 +398,8 @@ def _pmc_child(counters, batch, spec_file, per_channel, timeout, mode="static"):
                 d = agg.setdefault(r["Kernel_Name"], {}).setdefault(r["Counter_Name"], [])
                 d.append(float(r["Counter_Value"]))
         child = next((json.loads(ln) for ln in so.splitlines() if ln.startswith("{")), None)
+        if totals:
+            return {k: {c: [float(np.sum(v)), len(v)] for c, v in dd.items()} for k, dd in agg.items()}, child
         return {k: {c: float(np.mean(v)) for c, v in dd.items()} for k, dd in agg.items()}, child
     finally:
         shutil.rmtree(out, ignore_errors=True)
@@ -470,6 +478,8 @@ def pmc_counters(model, sd, args, names, timeout=150):
                     res[n]["clock_ghz"] = c["clock_ghz"]
                     res[n]["mfma_issue_at_clock"] = c["mfma_issue_at_clock"]
                     res[n]["clock_probe_ms"] = c["ms"]
+                if "phase_table" in c:
+                    res[n]["phase_table"] = c["phase_table"]
         except Exception as e:
             errors.append(f"clock: {e}")
     finally:
@@ -479,6 +489,140 @@ def pmc_counters(model, sd, args, names, timeout=150):
         if r.get("fetch_bytes") is not None and r.get("write_bytes") is not None:
             r["traffic_bytes"] = r["fetch_bytes"] + r["write_bytes"]
     return res, "; ".join(errors) or None
+
+
+class StepLoop:
+    """The timed step of the metric: one forward over this rank's resident
+    batch, plus at N > 1 the all-gather of its logits, issued asynchronously
+    (qconvnet.dist.gather_logits_async: RCCL runs it on its own stream behind
+    the batch's forward while the next batch computes into the model's other
+    buffer slot; a slot's gather is waited for before the slot is reused, and
+    every gather before the clock stops).  ``forward(marks=None, slot=0)``
+    launches one forward and returns its logits; ``sync`` waits for the device
+    (torch.cuda.synchronize; a no-op on CPU, where tests drive this loop over
+    gloo).  The timed regions are bracketed by a barrier and sync on both
+    sides and report the max over ranks."""
+
+    def __init__(self, forward, world, dev, sync=lambda: None, graph=False):
+        from qconvnet import dist as qd
+        self.qd, self.forward, self.world, self.dev = qd, forward, world, dev
+        self.sync, self.graph = sync, graph
+        self.gathered = None     # two [world * B, classes] buffers, allocated at the first step
+        self.pending = [None, None]
+        self.nstep = 0
+        self.last_slot = 0
+
+    def _tdev(self):
+        return self.dev if dist.get_backend() == "nccl" else "cpu"
+
+    def step(self, marks=None):
+        world = self.world
+        slot = self.nstep % 2 if world > 1 else 0
+        if self.pending[slot] is not None:
+            self.pending[slot].wait()
+            self.pending[slot] = None
+        logits = self.forward(marks=marks, slot=slot)
+        if world > 1:
+            if self.gathered is None:
+                self.gathered = [torch.empty((world * logits.shape[0],) + tuple(logits.shape[1:]),
+                                             dtype=logits.dtype, device=logits.device) for _ in range(2)]
+            self.pending[slot] = self.qd.gather_logits_async(logits, self.gathered[slot])
+            if self.graph:   # the graph has one logits buffer: done before the next replay
+                self.pending[slot].wait()
+                self.pending[slot] = None
+        self.last_slot = slot
+        self.nstep += 1
+        return logits
+
+    def drain(self):   # every outstanding all-gather has completed on the current stream
+        for i in range(2):
+            if self.pending[i] is not None:
+                self.pending[i].wait()
+                self.pending[i] = None
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def _max_over_ranks(self, v, dtype=torch.float64, op=None):
+        t = torch.tensor([v], dtype=dtype, device=self._tdev())
+        dist.all_reduce(t, op=op or dist.ReduceOp.MAX)
+        return t.item()
+
+    def timed(self, steps):
+        """Region A: ``steps`` back-to-back steps; returns (seconds = max over
+        ranks, every rank's ms per step or None at N = 1)."""
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.drain()
+        self.sync()
+        self.barrier()
+        elapsed = time.perf_counter() - t0
+        rank_ms = None
+        if self.world > 1:
+            # every rank's own step time (the spread separates slow ranks from the
+            # collective), then the max over ranks for the metric
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self._tdev())
+            allt = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.all_gather(allt, t)
+            rank_ms = [a.item() / steps * 1e3 for a in allt]
+            elapsed = max(a.item() for a in allt)
+        return elapsed, rank_ms
+
+    def sustained(self, per_step, steps, batch, seconds=1.0):
+        """Region S: the same step back to back for >= ``seconds`` right after
+        region A (a field beside the metric, never the metric)."""
+        n_sus = max(steps, int(np.ceil(seconds / max(per_step, 1e-6))))
+        if self.world > 1:
+            n_sus = int(self._max_over_ranks(n_sus, torch.int64))
+        self.barrier()
+        self.sync()
+        t0s = time.perf_counter()
+        for _ in range(n_sus):
+            self.step()
+        self.drain()
+        self.sync()
+        self.barrier()
+        el_s = time.perf_counter() - t0s
+        if self.world > 1:
+            el_s = float(self._max_over_ranks(el_s))
+        return {"value": self.world * batch * n_sus / el_s, "steps": n_sus, "seconds": el_s,
+                "ms_per_step": el_s / n_sus * 1e3,
+                "note": f"the same step back to back for >= {seconds:g} s right after the timed region; "
+                        "reported beside the metric, not as it"}
+
+    def allgather_timing(self, logits, reps):
+        """The logits all-gather on its own: a blocking all_gather_into_tensor of
+        one batch's logits, timed around device syncs (HIP events on the launch
+        stream on the GPU): the collective's latency as the timed step would see
+        it if nothing hid it."""
+        out = torch.empty((self.world * logits.shape[0],) + tuple(logits.shape[1:]), dtype=logits.dtype,
+                          device=logits.device)
+        gms = []
+        cuda = logits.is_cuda
+        for _ in range(reps):
+            self.barrier()
+            if cuda:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self.qd.gather_logits(logits, out)
+                e1.record()
+                self.sync()
+                gms.append(e0.elapsed_time(e1))
+            else:
+                self.sync()
+                t0 = time.perf_counter()
+                self.qd.gather_logits(logits, out)
+                self.sync()
+                gms.append((time.perf_counter() - t0) * 1e3)
+        return {"ms_mean": float(np.mean(gms)), "ms_min": float(np.min(gms)),
+                "bytes_per_rank": int(logits.numel() * logits.element_size()),
+                "note": "blocking all_gather_into_tensor of one batch's fp32 logits, HIP events "
+                        "on the launch stream; in the timed step it runs asynchronously behind "
+                        "the next batch's forward"}
 
 
 def main():
@@ -512,6 +656,10 @@ def main():
                     help="resnet50: split the batch over this many HIP streams, launches "
                          "interleaved layer by layer (QuantizedResNet.run_streams; measured "
                          "1/2/3/4: 81.7/86.7/86.3/72.1 K img/s at batch 512)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="convnet workload: skip the configs[1] / configs[4] child runs "
+                         "(configs_extra on the line)")
+    ap.add_argument("--extra-timeout", type=float, default=240.0)
     ap.add_argument("--workload", choices=("convnet", "qdq", "resnet50"), default="convnet",
                     help="convnet: BASELINE configs[2]/[3] (the metric); qdq: configs[1] (per-layer "
                          "QDQ CustomQuantizationModel, batch 256); resnet50: configs[4]")
@@ -536,39 +684,17 @@ def main():
     model, sd = build_model(rank, dev, args.per_channel, args.spec_file, mode)
     B = args.batch
     x = torch.from_numpy(data.synthetic_images(B, 100 + rank)).to(dev)
-    # N > 1: the logits all-gather of batch k runs while batch k+1 is computed
-    # (two logits buffers, model slots k % 2; the gather of batch k is waited
-    # for before slot k % 2 is reused, and all of them before the clock stops)
-    gathered = [torch.empty((world * B, 10), dtype=torch.float32, device=dev)
-                for _ in range(2)] if world > 1 else None
-    pending = [None, None]
-    nstep = [0]
-
     use_graph = args.graph
     if use_graph:   # the forward's launches as one HIP graph (same kernels, no launch gaps)
         model.capture_graph(x)
 
-    def step(marks=None):
-        slot = nstep[0] % 2 if world > 1 else 0
-        if pending[slot] is not None:
-            pending[slot].wait()
-            pending[slot] = None
+    def forward(marks=None, slot=0):
         if marks is None and use_graph:
-            logits = model.replay(B)
-        else:
-            logits = model.run(x, marks=marks, slot=slot)
-        if world > 1:
-            pending[slot] = qd.gather_logits_async(logits, gathered[slot])
-            if use_graph:   # the graph has one logits buffer: done before the next replay
-                pending[slot].wait()
-                pending[slot] = None
-        nstep[0] += 1
+            return model.replay(B)
+        return model.run(x, marks=marks, slot=slot)
 
-    def drain():   # every outstanding all-gather has completed on the current stream
-        for i in range(2):
-            if pending[i] is not None:
-                pending[i].wait()
-                pending[i] = None
+    loop = StepLoop(forward, world, dev, sync=torch.cuda.synchronize, graph=use_graph)
+    step, drain = loop.step, loop.drain
 
     def barrier():
         if world > 1:
@@ -577,55 +703,13 @@ def main():
     warm_run = ramp_warmup(step, drain, args.warmup, world, dev, args.warmup_min_ms * 1e-3)
 
     # ---- timed region A: the metric
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    rank_ms = None
-    if world > 1:
-        # every rank's own step time (the spread separates slow ranks from the
-        # collective), then the max over ranks for the metric
-        tdev = dev if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
-        allt = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(allt, t)
-        rank_ms = [a.item() / args.steps * 1e3 for a in allt]
-        elapsed = max(a.item() for a in allt)
+    elapsed, rank_ms = loop.timed(args.steps)
     images = world * B * args.steps
     value = images / elapsed
 
     # ---- region S: sustained throughput, >= 1 s of back-to-back steps (a
     # field beside the metric, never the metric: `value` is the K-step region)
-    per_step = elapsed / max(1, args.steps)
-    n_sus = max(args.steps, int(np.ceil(1.0 / max(per_step, 1e-6))))
-    if world > 1:
-        tdev = dev if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([n_sus], dtype=torch.int64, device=tdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        n_sus = int(t.item())
-    barrier()
-    torch.cuda.synchronize()
-    t0s = time.perf_counter()
-    for _ in range(n_sus):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    barrier()
-    el_s = time.perf_counter() - t0s
-    if world > 1:
-        tdev = dev if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([el_s], dtype=torch.float64, device=tdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_s = float(t.item())
-    sustained = {"value": world * B * n_sus / el_s, "steps": n_sus, "seconds": el_s,
-                 "ms_per_step": el_s / n_sus * 1e3,
-                 "note": "the same step back to back for >= 1 s right after the timed region; "
-                         "reported beside the metric, not as it"}
+    sustained = loop.sustained(elapsed / max(1, args.steps), args.steps, B)
 
     # ---- optional region C: batches in flight on several streams (serving)
     pipelined = None
@@ -678,21 +762,7 @@ def main():
     # collective's latency as the timed step would see it if nothing hid it)
     gather = None
     if world > 1:
-        logits = model.run(x)
-        gms = []
-        for _ in range(max(3, min(args.steps, 20))):
-            barrier()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            qd.gather_logits(logits, gathered[0])
-            e1.record()
-            torch.cuda.synchronize()
-            gms.append(e0.elapsed_time(e1))
-        gather = {"ms_mean": float(np.mean(gms)), "ms_min": float(np.min(gms)),
-                  "bytes_per_rank": int(logits.numel() * logits.element_size()),
-                  "note": "blocking all_gather_into_tensor of one batch's fp32 logits, HIP events "
-                          "on the launch stream; in the timed step it runs asynchronously behind "
-                          "the next batch's forward"}
+        gather = loop.allgather_timing(model.run(x), max(3, min(args.steps, 20)))
     dom = max(names, key=lambda n: kern[n]["ms"])
     k = kern[dom]
     if k["bound"] == "mfma":
@@ -763,6 +833,14 @@ def main():
         result["rank_ms_per_step"] = rank_ms
         result["rank_ms_spread"] = max(rank_ms) - min(rank_ms)
         result["allgather"] = gather
+    ph = kern.get("conv1_6", {}).get("phase_table")
+    if ph:
+        result["phases"] = {
+            "note": ("the one-launch conv1 .. conv6 phase by phase (SURVEY §8(d): conv4 and conv6 with "
+                     "every layer against its own bound): median workgroup cycles and us of each phase "
+                     "from the stamped diagnostic copy (tools/clock_probe.py), its MFMA cycles per SIMD, "
+                     "MFMA issue at the clock the chip holds in it, and frac = issue x clock / 2.4 GHz"),
+            **{k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in ph.items()}}
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baselines(sd, model, args.cpu_seconds)
         result["cpu_baseline"] = cb["static_ptq"]
@@ -772,11 +850,45 @@ def main():
             result["cpu_static_int8"] = cb["static_int8"]
         result["top1"] = cb["top1"]
         result["gpu_vs_cpu_ratio"] = value / cb["static_ptq"]["value"]
+    if rank == 0 and world == 1 and args.workload == "convnet" and not args.no_extra:
+        if under_profiler():
+            result["configs_extra"] = {"skipped": "this run is itself under rocprofv3: no child runs"}
+        else:
+            result["configs_extra"] = extra_configs(args)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def extra_configs(args):
+    """BASELINE configs[1] and configs[4] measured in the same run, each by its
+    own child `bench.py --workload ...` (same rules: resident synthetic input,
+    warmup, K timed steps; roofline with PMC traffic), so the driver's one
+    default run carries them.  Extra keys beside the metric, never it."""
+    out = {}
+    for key, wl in (("configs[1]", "qdq"), ("configs[4]", "resnet50")):
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--no-cpu"]
+        if args.no_pmc:
+            cmd.append("--no-pmc")
+        t0 = time.perf_counter()
+        try:
+            p = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                               timeout=args.extra_timeout)
+            line = next((ln for ln in p.stdout.splitlines() if ln.startswith("{")), None)
+            if p.returncode != 0 or line is None:
+                out[key] = {"error": f"exit {p.returncode}: {p.stderr[-300:]}"}
+                continue
+            d = json.loads(line)
+        except Exception as e:   # the metric above stands without these fields
+            out[key] = {"error": f"{type(e).__name__}: {e}"}
+            continue
+        keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "sustained", "config",
+                "roofline", "kernels", "launch_ms", "conv_gmac_per_image", "conv_algorithmic_bytes_per_image")
+        out[key] = {k: d[k] for k in keep if k in d}
+        out[key]["child_seconds"] = time.perf_counter() - t0
+    return out
 
 
 # ============================================================ configs[4]
@@ -816,6 +928,30 @@ def resnet_cpu_baseline(model_fp, seconds):
     out["fp32"]["sample"] = ("fp32 ResNet-50 (what CustomQuantizedResNet50 runs: its stubs are "
                              "never converted), " + out["fp32"]["sample"])
     return out, q
+
+
+RESNET_CONV_SYMBOLS = ("stem_fused_kernel", "conv_gemm_kernel", "conv1x1_stream_kernel", "conv3x3_img_kernel")
+
+
+def resnet_traffic(batch, timeout=240):
+    """HBM bytes per forward of the ResNet-50 conv launches (all four conv
+    kernel families): rocprofv3 --pmc passes over a single-stream child run
+    (FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction,
+    WRITE_SIZE as is), summed over the conv dispatches and divided by the
+    forwards the child ran (one stem dispatch each)."""
+    tot = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        agg, _ = _pmc_child((ctr,), batch, None, True, timeout, "resnet50",
+                            extra=("--workload", "resnet50", "--streams", "1"), totals=True)
+        fwd = next((v[ctr][1] for k, v in agg.items() if "stem_fused_kernel" in k and ctr in v), 0)
+        if not fwd:
+            raise RuntimeError(f"{ctr}: no stem dispatch counted")
+        kib = sum(v[ctr][0] for k, v in agg.items() if ctr in v and any(sy in k for sy in RESNET_CONV_SYMBOLS))
+        tot[ctr] = kib * 1024 / fwd * (2.0 if ctr == "FETCH_SIZE" else 1.0)
+    return {"traffic": tot["FETCH_SIZE"] + tot["WRITE_SIZE"], "fetch_bytes": tot["FETCH_SIZE"],
+            "write_bytes": tot["WRITE_SIZE"],
+            "traffic_note": "HBM bytes per forward of the conv launches (batch as on the line), from "
+                            "rocprofv3 --pmc passes of a single-stream child run: 2 x FETCH_SIZE + WRITE_SIZE"}
 
 
 def main_resnet(args):
@@ -877,6 +1013,23 @@ def main_resnet(args):
         sizes += ([ho * ho] if b["ds"] is not None else []) + [hh * hh, ho * ho, ho * ho]
         hh = ho
     mac_img = [sz * d.cout * d.w.shape[0] * 32 for sz, d in zip(sizes, convs)]  # K = chunks*32
+    # algorithmic HBM bytes per image of the conv launches, layer by layer: the
+    # stem reads the fp32 image and writes its max-pooled map; every other conv
+    # reads its u8 input map and writes its u8 output (the expand conv also
+    # reads the block's identity for the residual join)
+    hh = (x.shape[2] + 2 * convs[0].py - convs[0].kh) // convs[0].sy + 1
+    hh = (hh - 1) // 2 + 1
+    cin = convs[0].cout
+    conv_bytes = 3 * x.shape[2] * x.shape[3] * 4 + hh * hh * cin
+    for b in model.blocks:
+        ho = (hh + 2 * b["c2"].py - b["c2"].kh) // b["c2"].sy + 1
+        c1, c2, c3 = b["c1"].cout, b["c2"].cout, b["c3"].cout
+        if b["ds"] is not None:
+            conv_bytes += hh * hh * cin + ho * ho * c3
+        conv_bytes += hh * hh * cin + hh * hh * c1          # c1 (1x1)
+        conv_bytes += hh * hh * c1 + ho * ho * c2           # c2 (3x3, the block's stride)
+        conv_bytes += ho * ho * c2 + 2 * ho * ho * c3       # c3 (1x1) + identity read
+        hh, cin = ho, c3
     per_name = {}
     n_rep = max(3, min(args.steps, 10))
     conv_ms = []
@@ -896,8 +1049,17 @@ def main_resnet(args):
     tops = conv_ops / (conv_ms * 1e-3) / 1e12
     roof = {"kernel": "conv_gemm_kernel (all 53 conv launches)", "bound": "mfma", "achieved": tops,
             "peak": PEAK_INT8_TOPS, "unit": "TFLOP/s", "frac": tops / PEAK_INT8_TOPS, "traffic": None,
+            "algorithmic_bytes": conv_bytes * B,
             "note": "int8 TOPS in the TFLOP/s slot; achieved = 2*sum(conv MAC)*batch / summed "
                     "HIP-event conv time; stem MACs counted at the packed K=224 actually issued"}
+    if rank == 0 and world == 1 and not args.no_pmc:
+        if under_profiler():
+            roof["pmc_error"] = "skipped: this run is itself under rocprofv3"
+        else:
+            try:
+                roof.update(resnet_traffic(B))
+            except Exception as e:   # the fields stay null
+                roof["pmc_error"] = f"{type(e).__name__}: {e}"
     result = {
         "metric": METRIC_RESNET, "value": value, "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": warm_run,
@@ -911,6 +1073,7 @@ def main_resnet(args):
         "roofline": roof,
         "launch_ms": {k: round(float(np.sum(v) / n_rep), 4) for k, v in per_name.items()},
         "conv_gmac_per_image": sum(mac_img) / 1e9,
+        "conv_algorithmic_bytes_per_image": conv_bytes,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         cb, q_cpu = resnet_cpu_baseline(fp, args.cpu_seconds)

@@ -55,6 +55,11 @@
 #ifndef QCN_SM56_D
 #define QCN_SM56_D 4
 #endif
+// 1: the wave-specialised pair phases on v_mfma_i32_16x16x64_i8 (r05); 0
+// keeps the 32x32x32 pipeline for same-box A/B (diagnostic builds only)
+#ifndef QCN_M16
+#define QCN_M16 1
+#endif
 
 namespace qcn {
 
@@ -81,6 +86,7 @@ struct ConvCfg {
   // 2x2 quadrants) or 2 (64 pixels: row bands of the 56-wide ResNet maps)
   static constexpr int JT = JT_;
   static constexpr int MPS = JT * WI;            // MFMAs per K-step
+  static constexpr int kWpx = WPX;               // waves along the pixels
   static constexpr int WCO = COUT / (32 * WI);   // waves along cout
   static constexpr int NWAVES = WCO * WPX;
   static constexpr int NT = NWAVES * 64;         // threads
@@ -1269,12 +1275,13 @@ QCN_DEV void convpair_ws_body(int b, int G, const uint8_t* __restrict__ x, int n
   if (threadIdx.x < 64) p34_stamp(stamp_kind, stamp_i, __builtin_amdgcn_s_memrealtime());
 #endif
   P34_STAMP();
-  // tile k's input piece q of this A-role thread (images past the batch read
-  // the last image: their outputs are never stored)
+  // tile k's input piece q of this A-role thread (a phantom segment of a
+  // ragged last tile reads the tile's first image, which this workgroup owns:
+  // its outputs are never stored, and no other workgroup's bytes are read)
   auto in_src = [&](int k, int q) {
     const int p = rt + 256 * q;
     int n = img_of(k, p / (IMG * CH16));
-    n = n < nimg ? n : nimg - 1;
+    n = n < nimg ? n : img_of(k, 0);
     return x + ((long)n * IMG + (p / CH16) % IMG) * CA::kCin + (p % CH16) * 16;
   };
   auto in_dst = [&](int q) {
@@ -1520,6 +1527,414 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
   convpair_ws_body<CA, CB, D, FA, FB, KMAJOR>((int)blockIdx.x, (int)gridDim.x, x, nimg, x_zp, wa, epa, xb_zp,
                                               wb, epb, y);
 }
+
+// --------------------------------------------------------------------------
+// The wave-specialised pair on v_mfma_i32_16x16x64_i8 (r05).
+//
+// The 16x16x64 shape does the same MACs per cycle as 32x32x32, but under a
+// random-data int8 load the chip holds a higher clock with it: +11-18 % int8
+// TOP/s at equal operand bytes per MAC (tools/micro/mfma_shape2.hip,
+// profiles/r05_diag_mfma_shape.txt; r01's "2x slower" reading was a loop the
+// compiler had filled with accumulator moves).  The convs here are power
+// bound (DESIGN §5 "What bounds the convs"), so the shape is energy per image.
+//
+// Wave tile: 64 couts x 128 pixels as 4 x 8 blocks of 16 x 16; one K-step is
+// one 64-byte chunk (a tap's 64 input channels).  Lane l = (p = l % 16,
+// g = l / 16): A (weights, from L2) row 16 i + p, B (pixels, from the LDS
+// patch) pixel p of block j, both K bytes 16 g .. 16 g + 15 of the chunk; the
+// accumulator holds couts 16 i + 4 g + r (r = 0..3) of pixel p.  Pixel blocks:
+// rows of 16 output pixels (conv A), or for a pooled conv B block j = 4 gq + jq
+// is quadrant jq of pooled pixels 16 gq .. 16 gq + 15, so the 2x2 max is over
+// four blocks in registers.  The patch layouts are re-searched for these
+// reads (tools/lds_banks.py: every ds_read_b128 conflict-free needs a pixel
+// stride of 16 B x 2 mod 4, i.e. Cin + 32).
+
+// Patch slot of (wave wp, block j, lane pixel p) of conv C (output pixel
+// coordinates, the 3x3 taps add PatchAddr<C>::delta).  Every layout used is
+// affine: slot(wp, j, p) = slot(wp, 0, p) + jofs(j), checked at compile time,
+// so a lane holds one base address and the K loop reads at immediate offsets.
+template <class C>
+struct Pix16 {
+  static constexpr int slot(int seg, int prow, int pcol) {
+    const int cpos = C::kSplit ? ((pcol & 1) * C::HALF + (pcol >> 1)) : pcol;
+    return seg * C::SS + prow * C::RS + cpos * C::PS;
+  }
+  static constexpr int at(int wp, int j, int p) {
+    if (C::kPool) {
+      const int PW = C::W / 2, PR = C::R / 2;
+      const int q = wp * 32 + (j >> 2) * 16 + p, jq = j & 3;
+      return slot(q / (PR * PW), 2 * ((q / PW) % PR) + (jq >> 1), 2 * (q % PW) + (jq & 1));
+    }
+    const int m = (wp * 8 + j) * 16 + p;
+    return slot(m / (C::R * C::W), (m / C::W) % C::R, m % C::W);
+  }
+  // conv A's output pixel as an interior slot of the NEXT conv's patch (layout N)
+  template <class N>
+  static constexpr int out_at(int wp, int j, int p) {
+    const int m = (wp * 8 + j) * 16 + p;
+    return Pix16<N>::slot(m / (C::R * C::W), (m / C::W) % C::R + 1, m % C::W + 1);
+  }
+  static constexpr int jofs(int j) { return at(0, j, 0) - at(0, 0, 0); }
+  template <class N>
+  static constexpr int out_jofs(int j) { return out_at<N>(0, j, 0) - out_at<N>(0, 0, 0); }
+  static constexpr bool affine() {
+    for (int wp = 0; wp < C::kWpx; ++wp)
+      for (int j = 0; j < 8; ++j)
+        for (int p = 0; p < 16; ++p)
+          if (at(wp, j, p) != at(wp, 0, p) + jofs(j)) return false;
+    return true;
+  }
+  template <class N>
+  static constexpr bool out_affine() {
+    for (int wp = 0; wp < C::kWpx; ++wp)
+      for (int j = 0; j < 8; ++j)
+        for (int p = 0; p < 16; ++p)
+          if (out_at<N>(wp, j, p) != out_at<N>(wp, 0, p) + out_jofs<N>(j)) return false;
+    return true;
+  }
+};
+
+// One conv of the 16x16 pipeline over a staged patch: C::NCH K-steps of 32
+// MFMAs.  ga[s & 1] holds step s's four A fragments (step 0's issued by the
+// caller or by the previous job); step s + 1's are issued into the other slot
+// early in step s; after the last step the NEXT job's first chunk is issued
+// from wrn into slot 0 (its latency hides under the epilogue that follows).
+// B fragments are single-buffered: block j's fragment of step s + 1 is read
+// right after its fourth MFMA of step s.  lb: this lane's patch byte offset
+// (Pix16<C>::at(wp, 0, p) + 16 g); voff: ((wc 64 + p) 64 + 16 g).
+template <class C>
+QCN_DEV void pipe_job16(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_rsrc_t wrn, int voff, int wc,
+                        int lb, int g, v4i (&acc)[4][8], v4i (&ga)[2][4]) {
+  constexpr int CBK = C::kCin / 64, S = C::NCH;
+  using X = Pix16<C>;
+  static_assert(X::affine(), "pixel blocks at constant offsets");
+  v4i c0[4];   // the first K-step's C operand: the zero-point correction
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c0[i] = *reinterpret_cast<const v4i*>(corr + wc * 64 + 16 * i + 4 * g);
+  auto rd_b = [&](int s, int j) {
+    const int tap = s / CBK, cb = s % CBK;
+    return *reinterpret_cast<const v4i*>(patch + lb + X::jofs(j) + PatchAddr<C>::delta(tap, j) + cb * 64);
+  };
+  auto issue = [&](wt_rsrc_t r, int s, int slot) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, s * C::WBUF + i * 1024, 0);
+      ga[slot][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+    }
+  };
+  v4i fb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb[j] = rd_b(0, j);
+  static_for<S>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    static_for<32>([&](auto mc) {
+      constexpr int m = decltype(mc)::value, j = m >> 2, i = m & 3;
+      __builtin_amdgcn_sched_barrier(0);
+      acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ga[s & 1][i], fb[j], s == 0 ? c0[i] : acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (m == 1 && s + 1 < S) {
+        // slot (s + 1) & 1 was step s - 1's: all its MFMAs have issued
+        issue(wr, s + 1, (s + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (i == 3 && s + 1 < S) {
+        fb[j] = rd_b(s + 1, j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    // pin the step's MFMAs here (as pipe_job): side-effect free, they could
+    // otherwise be sunk towards their uses with the fragments held live
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(acc[i][j]));
+  });
+  issue(wrn, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <class CA, class CB>
+struct PairWs16 {
+  static_assert(CA::NWAVES == 4 && CB::NWAVES == 4 && CA::WCO == CB::WCO && CA::WI == 2 && CB::WI == 2,
+                "four waves of 64-cout x 128-pixel tiles per role");
+  static_assert(!CA::kPool && CB::kPool && CA::kCout == CB::kCin, "A feeds B");
+  static_assert(CA::PXB == CB::PXB && CA::SEGS == CB::SEGS && CA::R == CA::H && CA::W == CB::W &&
+                !CA::kBand && !CB::kBand && !CA::kSplit, "whole images per tile");
+  static_assert(Pix16<CA>::affine() && Pix16<CB>::affine() && Pix16<CA>::template out_affine<CB>(),
+                "pixel blocks at constant offsets");
+  static constexpr int SEGS = CA::SEGS, IMG = CA::IMG;
+  static constexpr int IN_BYTES = SEGS * IMG * CA::kCin;   // a tile's input
+  static_assert(IN_BYTES == 4 * 256 * 16, "four 16-B staging pieces per A-role thread");
+  static constexpr int PA = (CA::PATCH + 15) / 16 * 16, PB = (CB::PATCH + 15) / 16 * 16;
+  static constexpr int TAB = 16 * (CA::kCout + CB::kCout);   // u | v | mult | corr of both
+  static constexpr bool DOUBLE_A = 2 * PA + 2 * PB + TAB <= 160 * 1024;
+  static constexpr int OFF_PB = 0;
+  static constexpr int OFF_PA = 2 * PB;
+  static constexpr int OFF_EA = OFF_PA + (DOUBLE_A ? 2 : 1) * PA;   // u | v | mult, fp32 x cout each
+  static constexpr int OFF_EB = OFF_EA + 12 * CA::kCout;
+  static constexpr int OFF_CA = OFF_EB + 12 * CB::kCout;            // corr, int32 x cout
+  static constexpr int OFF_CB = OFF_CA + 4 * CA::kCout;
+  static constexpr int LDS = OFF_CB + 4 * CB::kCout;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static constexpr int OPI = CB::OPX / SEGS;   // pooled output pixels per image
+};
+
+// convpair_ws_body's schedule (roles, periods, LDS plan, tile -> image map
+// b, b + G, ... with ILV as there) on the 16x16 pipeline above.
+template <class CA, class CB, int FA, int FB, bool KMAJOR, bool ILV = false>
+QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int nimg, int x_zp,
+                                const int8_t* __restrict__ wa, const ConvEpi& epa, int xb_zp,
+                                const int8_t* __restrict__ wb, const ConvEpi& epb, uint8_t* __restrict__ y) {
+  using P = PairWs16<CA, CB>;
+  using XA = Pix16<CA>;
+  using XB = Pix16<CB>;
+  constexpr int SEGS = P::SEGS, IMG = CA::IMG, W = CA::W, WCO = CA::WCO;
+  constexpr int CH16 = CA::kCin / 16;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+  const int role = __builtin_amdgcn_readfirstlane(tid >> 8);   // 0: conv A, 1: conv B
+  const int rt = tid & 255, lane = tid & 63, wave = rt >> 6;   // thread / wave within the role
+  const int wc = wave % WCO, wp = wave / WCO;
+  int T;
+  if constexpr (ILV) {
+    const int mine = b < nimg ? (nimg - 1 - b) / G + 1 : 0;   // images b, b + G, ...
+    T = (mine + SEGS - 1) / SEGS;
+  } else {
+    const int ntile = (nimg + SEGS - 1) / SEGS;
+    T = b < ntile ? (ntile - 1 - b) / G + 1 : 0;   // this workgroup's tiles b, b + G, ...
+  }
+  // image of segment sg of tile k; a phantom segment of a ragged last tile
+  // (images past this workgroup's) maps to the tile's first image, which this
+  // workgroup owns: its outputs are never stored and no other workgroup's
+  // data is read
+  auto img_of = [&](int k, int sg) {
+    const int n = ILV ? b + (k * SEGS + sg) * G : (b + k * G) * SEGS + sg;
+    return n < nimg ? n : (ILV ? b + k * SEGS * G : (b + k * G) * SEGS);
+  };
+  auto in_src = [&](int k, int q) {
+    const int p = rt + 256 * q;
+    const int n = img_of(k, p / (IMG * CH16));
+    return x + ((long)n * IMG + (p / CH16) % IMG) * CA::kCin + (p % CH16) * 16;
+  };
+  auto in_dst = [&](int q) {
+    const int p = rt + 256 * q;
+    const int pix = (p / CH16) % IMG;
+    return CA::slot(p / (IMG * CH16), pix / W + 1, pix % W + 1) + (p % CH16) * 16;
+  };
+  uint4 sv[4];
+  if (role == 0 && T > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(0, q));
+  }
+  float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
+  float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
+  int* cra = reinterpret_cast<int*>(lds + P::OFF_CA);
+  int* crb = reinterpret_cast<int*>(lds + P::OFF_CB);
+  constexpr int NA = 3 * CA::kCout / 4, NB = 3 * CB::kCout / 4;       // float4 pieces
+  constexpr int NCA = CA::kCout / 4, NCB = CB::kCout / 4;
+  constexpr int NTAB = NA + NB + NCA + NCB, TPT = (NTAB + 255) / 256;
+  float4 tval[TPT];
+  auto tab = [&](int e, bool dst) -> float4* {
+    if (e < NA) {
+      const int a = e / (CA::kCout / 4), o = e % (CA::kCout / 4);
+      const float* s = a == 0 ? epa.u : (a == 1 ? epa.v : epa.mult);
+      return dst ? reinterpret_cast<float4*>(eka) + e : const_cast<float4*>(reinterpret_cast<const float4*>(s) + o);
+    }
+    e -= NA;
+    if (e < NB) {
+      const int a = e / (CB::kCout / 4), o = e % (CB::kCout / 4);
+      const float* s = a == 0 ? epb.u : (a == 1 ? epb.v : epb.mult);
+      return dst ? reinterpret_cast<float4*>(ekb) + e : const_cast<float4*>(reinterpret_cast<const float4*>(s) + o);
+    }
+    e -= NB;
+    if (e < NCA)
+      return dst ? reinterpret_cast<float4*>(cra) + e
+                 : const_cast<float4*>(reinterpret_cast<const float4*>(epa.corr) + e);
+    e -= NCA;
+    return dst ? reinterpret_cast<float4*>(crb) + e
+               : const_cast<float4*>(reinterpret_cast<const float4*>(epb.corr) + e);
+  };
+  if (role == 1) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (rt + 256 * k < NTAB) tval[k] = *tab(rt + 256 * k, false);
+  }
+  {  // zero-point halos of every buffer of both patches (never overwritten)
+    const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
+    auto halo = [&](auto cfg, uint8_t* base, int nbuf, int pbytes, uint32_t pad) {
+      using C = decltype(cfg);
+      constexpr int HS = 2 * C::PCOLS + 2 * (C::PROWS - 2), CH = C::kCin / 16;
+      const int total = nbuf * C::SEGS * HS * CH;
+      for (int e = tid; e < total; e += 512) {
+        const int c = e % CH, hs = (e / CH) % HS, sg = (e / (CH * HS)) % C::SEGS, bf = e / (CH * HS * C::SEGS);
+        int pr, pc;
+        if (hs < C::PCOLS) { pr = 0; pc = hs; }
+        else if (hs < 2 * C::PCOLS) { pr = C::PROWS - 1; pc = hs - C::PCOLS; }
+        else { const int r = hs - 2 * C::PCOLS; pr = 1 + (r >> 1); pc = (r & 1) ? C::PCOLS - 1 : 0; }
+        *reinterpret_cast<uint4*>(base + bf * pbytes + C::slot(sg, pr, pc) + c * 16) = make_uint4(pad, pad, pad, pad);
+      }
+    };
+    halo(CA{}, lds + P::OFF_PA, P::DOUBLE_A ? 2 : 1, P::PA, pa4);
+    halo(CB{}, lds + P::OFF_PB, 2, P::PB, pb4);
+  }
+  if (role == 1) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (rt + 256 * k < NTAB) *tab(rt + 256 * k, true) = tval[k];
+  }
+  if (T == 0) return;   // (uniform; the launcher never makes such a workgroup)
+
+  const int p16 = lane & 15, g = lane >> 4;
+  const wt_rsrc_t wra = wt_rsrc(wa), wrb = wt_rsrc(wb);
+  const int voff = (wc * 64 + p16) * 64 + g * 16;
+  auto pa_buf = [&](int j) { return lds + P::OFF_PA + (P::DOUBLE_A ? (j & 1) * P::PA : 0); };
+  auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
+  auto write_in = [&](uint8_t* pa) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<uint4*>(pa + in_dst(q)) =
+          make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
+  };
+
+  v4i acc[4][8];
+  v4i ga[2][4];
+  {
+    const wt_rsrc_t w0 = role == 0 ? wra : wrb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(w0, voff, i * 1024, 0);
+      ga[0][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+    }
+  }
+  if (role == 0) write_in(pa_buf(0));
+  lds_barrier();
+
+  // lane-derived addressing from a laundered lane id (not hoisted out of the
+  // period loop and held live across the MFMA jobs)
+  struct Lane {
+    int p16, g, ek;
+    int la, lb;   // patch offsets of block 0: conv A's and conv B's B-fragment reads
+    int hb;       // conv B patch slot of conv A's output pixel (block 0) + this lane's channels
+    int q;        // pooled output pixel of conv B within the tile (block group 0)
+    const int *ca, *cb;
+  };
+  auto lanes = [&]() {
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    Lane L;
+    L.p16 = lz & 15;
+    L.g = lz >> 4;
+    L.ek = wc * 64 + 4 * L.g;
+    L.la = XA::at(wp, 0, L.p16) + 16 * L.g;
+    L.lb = XB::at(wp, 0, L.p16) + 16 * L.g;
+    L.hb = XA::template out_at<CB>(wp, 0, L.p16) + wc * 64 + 4 * L.g;
+    L.q = wp * 32 + L.p16;
+    L.ca = cra + (lz >> 6);   // (lz >> 6 == 0: an address the compiler cannot hoist)
+    L.cb = crb + (lz >> 6);
+    return L;
+  };
+  // A's epilogue into B's patch pb: one dword (4 channels) per block and row
+  // of 16 channels, at the block's constant offset
+  auto epi_a = [&](const Lane& L, uint8_t* pb) {
+    static_for<4>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const EpiG K = load_epig(eka, CA::kCout, L.ek + 16 * i);
+      static_for<8>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        uint32_t wd = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wd = rq_elem<FA>(acc[i][j][r], K, r, epa, wd);
+        *reinterpret_cast<uint32_t*>(pb + L.hb + XA::template out_jofs<CB>(j) + 16 * i) = xor80(wd);
+      });
+    });
+  };
+  // B's pooled epilogue of tile k: per group of 16 pooled pixels, the max over
+  // the four quadrant blocks, requant, a 4 x 4 dword transpose across the lane
+  // groups (two permlane32 + two permlane16 swaps) and one 16-B store per lane
+  auto epi_b = [&](const Lane& L, int k) {
+    static_for<2>([&](auto gc) {
+      constexpr int gq = decltype(gc)::value;
+      uint32_t d[4];
+      static_for<4>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const EpiG K = load_epig(ekb, CB::kCout, L.ek + 16 * i);
+        uint32_t wd = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = max(max(acc[i][4 * gq][r], acc[i][4 * gq + 1][r]),
+                            max(acc[i][4 * gq + 2][r], acc[i][4 * gq + 3][r]));
+          wd = rq_elem<FB>(a, K, r, epb, wd);
+        }
+        d[i] = wd;
+      });
+      const auto s02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+      const auto s13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+      const auto t01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+      const auto t23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+      const uint4 v = make_uint4(t01[0], t01[1], t23[0], t23[1]);   // channels co .. co + 15
+      const int q = L.q + 16 * gq;
+      const int n = img_of(k, q / P::OPI), pix = q % P::OPI;
+      const int co = wc * 64 + 16 * L.g;
+      const bool real = ILV ? b + (k * SEGS + q / P::OPI) * G < nimg : (b + k * G) * SEGS + q / P::OPI < nimg;
+      if (real) {
+        if constexpr (KMAJOR) {   // [f / 32][image][32], f = pix * cout + channel (NHWC flatten)
+          const int kc = (pix * CB::kCout + co) / 32;
+          store_wt16(wt_rsrc(y), (uint32_t)(((long)kc * nimg + n) * 32 + 16 * (L.g & 1)), v);
+        } else {
+          store_wt16(wt_rsrc(y + (long)n * P::OPI * CB::kCout), (uint32_t)(pix * CB::kCout + co), v);
+        }
+      }
+    });
+  };
+
+  if (role == 0) {
+#pragma unroll 1
+    for (int p = 0; p <= T; ++p) {
+      if constexpr (!P::DOUBLE_A) {   // tile p's input, held since period p - 1
+        if (p >= 1 && p < T) write_in(pa_buf(p));
+        lds_barrier();
+      }
+      if (p < T) {
+        const Lane L = lanes();
+        pipe_job16<CA>(pa_buf(p), L.ca, wra, wra, voff, wc, L.la, L.g, acc, ga);
+        const int kn = p + 1 < T ? p + 1 : p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(kn, q));
+        epi_a(L, pb_buf(p));
+        if constexpr (P::DOUBLE_A) write_in(pa_buf(p + 1));
+      }
+      lds_barrier();
+    }
+  } else {
+#pragma unroll 1
+    for (int p = 0; p <= T; ++p) {
+      if constexpr (!P::DOUBLE_A) lds_barrier();
+      if (p >= 1) {
+        const Lane L = lanes();
+        if (p >= 2) epi_b(L, p - 2);
+        pipe_job16<CB>(pb_buf(p - 1), L.cb, wrb, wrb, voff, wc, L.lb, L.g, acc, ga);
+      }
+      lds_barrier();
+    }
+    const Lane L = lanes();
+    epi_b(L, T - 1);
+  }
+}
+
+template <class CA, class CB, int FA, int FB, bool KMAJOR>
+__global__ __launch_bounds__(512, 1)
+void convpair_ws16_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const int8_t* __restrict__ wa,
+                          ConvEpi epa, int xb_zp, const int8_t* __restrict__ wb, ConvEpi epb,
+                          uint8_t* __restrict__ y) {
+  convpair_ws16_body<CA, CB, FA, FB, KMAJOR>((int)blockIdx.x, (int)gridDim.x, x, nimg, x_zp, wa, epa, xb_zp,
+                                             wb, epb, y);
+}
+
+// The headline's patch layouts for the 16x16 reads (tools/lds_banks.py)
+using W16A3 = ConvCfg<64, 128, 16, false, 2, 32, 0, 0, false>;
+using W16B4 = ConvCfg<128, 128, 16, true, 2, 32, 64, 0, true>;
+using W16A5 = ConvCfg<128, 256, 8, false, 1, 32, 192, 0, false>;
+using W16B6 = ConvCfg<256, 256, 8, true, 1, 32, 0, 0, true>;
 
 // --------------------------------------------------------------------------
 // conv1: CIN = 3, input fp32 NCHW quantized on the fly (aten quantize_per_tensor
@@ -2144,8 +2559,9 @@ using WsA5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
 using WsB6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE34_D>::LDS,
+[[maybe_unused]] constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE34_D>::LDS,
                                                    PairWs<WsA5, WsB6, QCN_PIPE34_D>::LDS));
+[[maybe_unused]] constexpr int kConvnet16Lds = cmax(Conv12P::LDS, cmax(PairWs16<W16A3, W16B4>::LDS, PairWs16<W16A5, W16B6>::LDS));
 constexpr int kConvnetSmLds = cmax(Conv12P::LDS, cmax(PairCfg<SmA3, SmB4>::LDS, PairGaCfg<SmA5, SmB6>::LDS));
 
 // Diagnostic builds only (tools/clock: -DQCN_CONVNET_STAMP): s_memtime /
@@ -2180,6 +2596,9 @@ template <int EM, bool KMAJOR>
 __global__ __launch_bounds__(512, 1)
 void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, QCN_C16_PARAMS,
                           uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
+  // conv3+4 (ILV false) reads only its own workgroup's a2 because its tiles
+  // are single images: tile b + kG is image b + kG, as conv12p wrote it
+  static_assert(PairWs<WsA3, WsB4, QCN_PIPE34_D>::SEGS == 1, "conv3+4 tile k of workgroup b is image b + kG");
   const int b = (int)blockIdx.x, G = (int)gridDim.x;
   const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
   C16_STAMP(0);
@@ -2190,6 +2609,31 @@ void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, Q
   phase_boundary();
   C16_STAMP(2);
   convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
+#ifdef QCN_CONVNET_STAMP
+  __syncthreads();
+#endif
+  C16_STAMP(3);
+}
+
+// The same launch with the pair phases on the 16x16x64 pipeline (r05).  The
+// conv12 phase is unchanged.  Each pair phase reads only a2 / a4 images its
+// own workgroup wrote (conv3+4 tiles b, b + G, ... of one image each —
+// static_assert below — and conv5+6 the interleaved pairs).
+template <int EM, bool KMAJOR>
+__global__ __launch_bounds__(512, 1)
+void convnet_convs16_kernel(const float* __restrict__ x, int nimg, float in_inv, QCN_C16_PARAMS,
+                            uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
+  static_assert(PairWs16<W16A3, W16B4>::SEGS == 1, "conv3+4 tile k of workgroup b is image b + kG");
+  const int b = (int)blockIdx.x, G = (int)gridDim.x;
+  const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
+  C16_STAMP(0);
+  conv12p_body(b, G, T, x, nimg, in_inv, z0, w0, e0, z1, w1, e1, a2);
+  phase_boundary();
+  C16_STAMP(1);
+  convpair_ws16_body<W16A3, W16B4, EM, EM, false>(b, G, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
+  phase_boundary();
+  C16_STAMP(2);
+  convpair_ws16_body<W16A5, W16B6, EM, EM, KMAJOR, true>(b, G, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif
@@ -2354,6 +2798,7 @@ void set_qdq(ConvEpi& ep, const qcn_qdq_t* q) {
 
 }  // namespace qcn
 
+#ifndef QCN_NO_ABI   // (defined only by single-kernel diagnostic translation units)
 // ==========================================================================
 // C-ABI dispatch
 // ==========================================================================
@@ -2415,7 +2860,20 @@ int launch_pair_ws_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, con
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-template <class CA, class CB, int D>
+template <class CA, class CB, int FA, int FB, bool KM>
+int launch_pair_ws16_k(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
+                       const int8_t* wb, const ConvEpi& epb, uint8_t* y, hipStream_t st, int ncu) {
+  using P = PairWs16<CA, CB>;
+  auto k = convpair_ws16_kernel<CA, CB, FA, FB, KM>;
+  static bool attr_done[QCN_MAX_DEV] = {};
+  if (!qcn_set_lds_once((const void*)k, P::LDS, attr_done)) return QCN_ERR_HIP;
+  const int ntile = (nimg + P::SEGS - 1) / P::SEGS;
+  const int grid = ntile < ncu ? ntile : ncu;   // persistent: one workgroup per CU
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), P::LDS, st, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
+  return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+template <class CA, class CB, int D, class CA16 = void, class CB16 = void>
 int launch_pair_ws(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const ConvEpi& epa, int xb_zp,
                    const int8_t* wb, const ConvEpi& epb, bool kmajor, uint8_t* y, hipStream_t st, int ncu) {
   // epilogue modes, known on the host: 1 the FBGEMM fast path (zp_y == 0, no
@@ -2423,6 +2881,16 @@ int launch_pair_ws(const uint8_t* x, int nimg, int x_zp, const int8_t* wa, const
   // net), 0 general
   int fa = epi_mode(epa), fb = epi_mode(epb);
   if ((fa == 2) != (fb == 2)) { fa = fa == 2 ? 0 : fa; fb = fb == 2 ? 0 : fb; }
+  // the 16x16 forms for the two epilogue pairs the nets use (both convs on
+  // the FBGEMM fast path, or both on the one-fma QDQ form); mixed forms stay
+  // on the 32x32 kernel (results are identical: exact integer arithmetic)
+  if constexpr (!std::is_void_v<CA16>) {
+#define QCN_WS16(FA_, FB_, KM_)                                                                      \
+  if (fa == FA_ && fb == FB_ && kmajor == KM_)                                                       \
+    return launch_pair_ws16_k<CA16, CB16, FA_, FB_, KM_>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
+    QCN_WS16(1, 1, false) QCN_WS16(2, 2, false) QCN_WS16(1, 1, true) QCN_WS16(2, 2, true)
+#undef QCN_WS16
+  }
 #define QCN_WS(FA_, FB_, KM_) \
   if (fa == FA_ && fb == FB_ && kmajor == KM_)                                                            \
     return launch_pair_ws_k<CA, CB, D, FA_, FB_, KM_>(x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y, st, ncu);
@@ -2589,9 +3057,13 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     using A3 = WsA3;
     using B4 = WsB4;
     // two or more images per CU: the persistent wave-specialised kernel
-    if (QCN_WS34 && nimg >= 2 * ncu)
+    if (QCN_WS34 && nimg >= 2 * ncu) {
+      if (QCN_M16)
+        return launch_pair_ws<A3, B4, QCN_PIPE34_D, W16A3, W16B4>(x, nimg, x_zp, wa_packed, epa, xb_zp,
+                                                                  wb_packed, epb, kmajor != 0, y, st, ncu);
       return launch_pair_ws<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
                                                   kmajor != 0, y, st, ncu);
+    }
     return launch_pair<A3, B4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
@@ -2613,9 +3085,13 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
       return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // two or more image pairs per CU: the persistent wave-specialised kernel
-    if (QCN_WS56 && nimg >= 4 * ncu)
+    if (QCN_WS56 && nimg >= 4 * ncu) {
+      if (QCN_M16)
+        return launch_pair_ws<A1, B1, QCN_PIPE34_D, W16A5, W16B6>(x, nimg, x_zp, wa_packed, epa, xb_zp,
+                                                                  wb_packed, epb, kmajor != 0, y, st, ncu);
       return launch_pair_ws<A1, B1, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
                                                   kmajor != 0, y, st, ncu);
+    }
     return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;
@@ -2694,39 +3170,38 @@ int qcn_conv12_fused_f32_nchw(const float* x, int nimg, float in_scale, int in_z
   return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
-int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
-                               const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
-                               int kmajor, void* stream) {
-  if (!x || !layers || !a2 || !a4 || !a6) return QCN_ERR_ARG;
+}  // extern "C"
+
+namespace {
+// The form qcn_convnet_convs_f32_nchw takes (shared with the host query
+// qcn_convnet_convs_form): fills L and the epilogue mode em and returns 1 (one
+// image per workgroup), 2 (persistent) or the error the launch returns.
+int convnet_convs_plan(int nimg, float in_scale, int in_zp, const qcn_conv_layer_t* layers, int kmajor,
+                       qcn::ConvnetLayers& L, int& em, int& ncu) {
+  if (!layers) return QCN_ERR_ARG;
   if (nimg <= 0 || in_zp < 0 || in_zp > 255 || !(in_scale > 0.f)) return QCN_ERR_ARG;
-  qcn::ConvnetLayers L{};
+  L = qcn::ConvnetLayers{};
   for (int i = 0; i < 6; ++i) {
     const qcn_conv_layer_t& l = layers[i];
     if (!l.w || !l.u || !l.v || !l.mult || !l.corr) return QCN_ERR_ARG;
     if (l.x_zp < 0 || l.x_zp > 255 || l.y_zp < 0 || l.y_zp > 255) return QCN_ERR_ARG;
+    // conv i reads conv i-1's output: its input zero point is that layer's
+    // output zero point, or the z2 of that layer's QDQ hand-off
+    if (i > 0 && l.x_zp != (layers[i - 1].qdq ? layers[i - 1].qdq->z2 : layers[i - 1].y_zp)) return QCN_ERR_ARG;
     L.w[i] = l.w;
-    L.ep[i] = ConvEpi{l.u, l.v, l.mult, l.corr, l.y_zp, l.relu ? l.y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
+    L.ep[i] = qcn::ConvEpi{l.u, l.v, l.mult, l.corr, l.y_zp, l.relu ? l.y_zp : 0, 0, 0.f, 0, 0.f, 0, 0};
     if (l.qdq) qcn::set_qdq(L.ep[i], l.qdq);
     L.x_zp[i] = l.x_zp;
   }
   if (L.x_zp[0] != in_zp) return QCN_ERR_ARG;
   L.ep[5].kmajor = kmajor ? 1 : 0;
   if ((long)nimg * 4096 > 0x7fffffffL) return QCN_ERR_UNSUPPORTED;   // 32-bit store offsets
-  const int ncu = qcn_cu_count();
+  ncu = qcn_cu_count();
   if (ncu <= 0) return QCN_ERR_HIP;
-  const float inv = 1.0f / in_scale;
-  if (nimg <= ncu) {   // one image per workgroup
-    static bool sm_done[QCN_MAX_DEV] = {};
-    if (!qcn_set_lds_once((const void*)qcn::convnet_convs_sm_kernel, qcn::kConvnetSmLds, sm_done))
-      return QCN_ERR_HIP;
-    hipLaunchKernelGGL(qcn::convnet_convs_sm_kernel, dim3(nimg), dim3(512), qcn::kConvnetSmLds,
-                       (hipStream_t)stream, x, nimg, inv, QCN_C16_ARGS(L), a2, a4, a6);
-    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
-  }
+  if (nimg <= ncu) return 1;   // one image per workgroup
   // the two pair phases are the wave-specialised kernels of >= 4 images per CU;
   // conv3..conv6 all on the FBGEMM fast epilogue or all on the one-fma QDQ form
   if (nimg < 4 * ncu) return QCN_ERR_UNSUPPORTED;
-  int em = -1;
   bool all1 = true, all2 = true;
   for (int i = 2; i < 6; ++i) {
     all1 = all1 && qcn::epi_mode(L.ep[i]) == 1;
@@ -2735,18 +3210,56 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
   if (all1) em = 1;
   else if (all2) em = 2;
   else return QCN_ERR_UNSUPPORTED;
+  return 2;
+}
+}  // namespace
+
+extern "C" {
+
+int qcn_convnet_convs_form(int nimg, float in_scale, int in_zp, const qcn_conv_layer_t* layers, int kmajor) {
+  qcn::ConvnetLayers L;
+  int em = 0, ncu = 0;
+  return convnet_convs_plan(nimg, in_scale, in_zp, layers, kmajor, L, em, ncu);
+}
+
+int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
+                               const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
+                               int kmajor, void* stream) {
+  if (!x || !layers || !a2 || !a4 || !a6) return QCN_ERR_ARG;
+  qcn::ConvnetLayers L;
+  int em = 0, ncu = 0;
+  const int form = convnet_convs_plan(nimg, in_scale, in_zp, layers, kmajor, L, em, ncu);
+  if (form < 0) return form;
+  const float inv = 1.0f / in_scale;
+  if (form == 1) {   // one image per workgroup
+    static bool sm_done[QCN_MAX_DEV] = {};
+    if (!qcn_set_lds_once((const void*)qcn::convnet_convs_sm_kernel, qcn::kConvnetSmLds, sm_done))
+      return QCN_ERR_HIP;
+    hipLaunchKernelGGL(qcn::convnet_convs_sm_kernel, dim3(nimg), dim3(512), qcn::kConvnetSmLds,
+                       (hipStream_t)stream, x, nimg, inv, QCN_C16_ARGS(L), a2, a4, a6);
+    return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+  }
   static bool attr_done[4][QCN_MAX_DEV] = {};
+#if QCN_M16
+#define QCN_C16_KERNEL qcn::convnet_convs16_kernel
+#define QCN_C16_LDS qcn::kConvnet16Lds
+#else
+#define QCN_C16_KERNEL qcn::convnet_convs_kernel
+#define QCN_C16_LDS qcn::kConvnetLds
+#endif
 #define QCN_C16(EM_, KM_)                                                                          \
   if (em == EM_ && (kmajor != 0) == KM_) {                                                         \
-    auto k = qcn::convnet_convs_kernel<EM_, KM_>;                                                  \
-    if (!qcn_set_lds_once((const void*)k, qcn::kConvnetLds, attr_done[(EM_ - 1) * 2 + KM_]))       \
+    auto k = QCN_C16_KERNEL<EM_, KM_>;                                                             \
+    if (!qcn_set_lds_once((const void*)k, QCN_C16_LDS, attr_done[(EM_ - 1) * 2 + KM_]))            \
       return QCN_ERR_HIP;                                                                          \
-    hipLaunchKernelGGL(k, dim3(ncu), dim3(512), qcn::kConvnetLds, (hipStream_t)stream, x, nimg, inv, \
+    hipLaunchKernelGGL(k, dim3(ncu), dim3(512), QCN_C16_LDS, (hipStream_t)stream, x, nimg, inv,    \
                        QCN_C16_ARGS(L), a2, a4, a6);                                               \
     return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;                                 \
   }
   QCN_C16(1, true) QCN_C16(1, false) QCN_C16(2, true) QCN_C16(2, false)
 #undef QCN_C16
+#undef QCN_C16_KERNEL
+#undef QCN_C16_LDS
   return QCN_ERR_UNSUPPORTED;
 }
 
@@ -2780,3 +3293,4 @@ int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_
 }
 
 }  // extern "C"
+#endif  // QCN_NO_ABI

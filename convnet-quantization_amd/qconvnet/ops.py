@@ -211,6 +211,18 @@ def convnet_convs(x, in_scale, in_zp, layers, a2, a4, a6, kmajor=True):
     return True
 
 
+def convnet_convs_form(n, in_scale, in_zp, layers, kmajor=True):
+    """Host query (no launch, current device): 1 when convnet_convs() runs one
+    image per workgroup for batch n, 2 the persistent form, 0 when it would
+    return False (the three launches run instead)."""
+    rc = lib().qcn_convnet_convs_form(int(n), float(in_scale), int(in_zp), layers, int(bool(kmajor)))
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return 0
+    if rc < 0:
+        check(rc, "convnet_convs_form")
+    return rc
+
+
 def linear_u8(x, x_zp, w, u, v, mult, corr, y_zp, relu, y_scale=0.0, want_fp32=False, out=None,
               out_f=None):
     _need(x, torch.uint8, "linear.x")

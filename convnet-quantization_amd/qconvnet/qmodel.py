@@ -308,7 +308,7 @@ class QuantizedConvNet:
         """Names of the launches run() marks, in order (conv1+conv2 are one
         launch when fused, conv3+conv4 / conv5+conv6 one launch each when
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
-        if self._convs(x_shape, keep) and self._convs_ok.get(x_shape[0]):
+        if self._convs(x_shape, keep) and self._convs_form(x_shape[0], keep):
             return ("conv1_6", "fc12") if self._head(x_shape[0], keep) else ("conv1_6", "fc1", "fc2")
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
         if self._pairs(keep):
@@ -342,6 +342,19 @@ class QuantizedConvNet:
 
     def _fused(self, x_shape):
         return self.fuse12 and tuple(x_shape[1:]) == (3, 32, 32)
+
+    def _convs_form(self, n, keep=False):
+        """Whether the library takes the one-launch convs at batch n: what a
+        run() recorded, else the library's host query (no launch), so
+        kernel_names() is right before the first forward at a batch size."""
+        ok = self._convs_ok.get(n)
+        if ok is None:
+            if self._conv_layers is None:
+                self._conv_layers = ops.conv_layers(self.L, self.in_zp)
+            with torch.cuda.device(self.device):
+                ok = ops.convnet_convs_form(n, self.in_scale, self.in_zp, self._conv_layers,
+                                            kmajor=self._head(n, keep)) > 0
+        return ok
 
     def _convs(self, x_shape, keep):
         """The one-launch conv1 .. conv6 applies to this forward (the library

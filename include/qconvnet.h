@@ -116,10 +116,6 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
                           const float* mult, const int32_t* corr, int y_zp, int relu, int pool,
                           const qcn_qdq_t* qdq, uint8_t* y, void* stream);
 
-/* A1+A5+A6 fused — QuantStub + conv1(+ReLU) of SimpleConvNet
- * (baseline_model.py:13, :60): fp32 NCHW [nimg,3,hw,hw] in, quantized with
- * (in_scale, in_zp), 3x3 conv to 64 channels, u8 NHWC out.  q_in (optional,
- * may be NULL) receives the quantized input, u8 NHWC. */
 /* A1 + conv1 .. conv6 of SimpleConvNet (baseline_model.py:60-72; per-layer
  * QDQ form custom_quantization_model.py:233-255) in ONE persistent launch:
  * fp32 NCHW [nimg,3,32,32] in (quantized with in_scale / in_zp ==
@@ -129,11 +125,28 @@ int qcn_conv3x3_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int
  * written on the way.  Each workgroup carries its own
  * images through all six convs, so the results are those of
  * qcn_conv12_fused_f32_nchw + two qcn_conv3x3_pair_u8s8 launches bit for
- * bit.  QCN_ERR_UNSUPPORTED when nimg < 4 x CUs or conv3..conv6 are not all
- * on the same fast epilogue (the caller then launches the three kernels). */
+ * bit.  By batch, with C = the device's CUs:
+ *   nimg <= C        one image per workgroup (convnet_convs_sm_kernel);
+ *   C < nimg < 4 C   QCN_ERR_UNSUPPORTED (the caller launches the three kernels);
+ *   nimg >= 4 C      one persistent workgroup per CU, when conv3..conv6 are all
+ *                    on the FBGEMM fast epilogue or all on the one-fma QDQ form
+ *                    (else QCN_ERR_UNSUPPORTED).
+ * layers[i].x_zp must be conv i-1's output zero point (its QDQ hand-off's z2
+ * when it has one): QCN_ERR_ARG otherwise. */
 int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_zp,
                                const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
                                int kmajor, void* stream);
+
+/* Host query (no launch): which form qcn_convnet_convs_f32_nchw takes for
+ * these arguments on the current device — 1 one image per workgroup, 2 the
+ * persistent form, or the error it would return (QCN_ERR_UNSUPPORTED,
+ * QCN_ERR_ARG, QCN_ERR_HIP). */
+int qcn_convnet_convs_form(int nimg, float in_scale, int in_zp, const qcn_conv_layer_t* layers, int kmajor);
+
+/* A1+A5+A6 fused — QuantStub + conv1(+ReLU) of SimpleConvNet
+ * (baseline_model.py:13, :60): fp32 NCHW [nimg,3,hw,hw] in, quantized with
+ * (in_scale, in_zp), 3x3 conv to 64 channels, u8 NHWC out.  q_in (optional,
+ * may be NULL) receives the quantized input, u8 NHWC. */
 int qcn_conv1_f32_nchw(const float* x, int nimg, int hw, float in_scale, int in_zp,
                        const int8_t* w1_packed, const float* u, const float* v, const float* mult,
                        const int32_t* corr, int y_zp, int relu, const qcn_qdq_t* qdq, uint8_t* y,

@@ -5,7 +5,7 @@ set -e
 A=$1; B=$2; N=${3:-3}
 for i in $(seq $N); do
   for E in "$A" "$B"; do
-    env $E timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu --no-pmc 2>/dev/null | python -c "
+    env $E timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu --no-pmc --no-extra 2>/dev/null | python -c "
 import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']
 print('%-36s %9.0f img/s  ' % ('[$E]'[-36:], d['value']) + ' '.join('%s=%.1f' % (n, v['ms']*1e3) for n, v in k.items()))"
   done

@@ -22,7 +22,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DIAG_LIB = os.path.join(ROOT, "tools", "clock", "libqconvnet_clock.so")
+DIAG_LIB = os.environ.get("QCN_CLOCK_LIB", os.path.join(ROOT, "tools", "clock", "libqconvnet_clock.so"))
 os.environ["QCN_LIB"] = DIAG_LIB   # before qconvnet is imported
 for _p in (os.path.join(ROOT, "convnet-quantization_amd"), ROOT):
     if _p not in sys.path:
@@ -126,9 +126,30 @@ def main():
                 b16 = np.zeros((g, 8), np.uint64)
                 _lib.check(fn16(b16.ctypes.data, g), "qcn_clock_read_c16")
                 t = b16[:, :4].astype(np.float64)
+                r = b16[:, 4:].astype(np.float64)
                 rec["phase_cycles_median"] = {
                     ph: float(np.median(t[:, i + 1] - t[:, i]))
                     for i, ph in enumerate(("conv12", "conv34", "conv56"))}
+                # every phase against its own bound.  A phase's MFMA
+                # cycles per SIMD are its images' MACs over the workgroup's 4
+                # SIMDs at 1024 MAC / clk; issue = those / the phase's cycles (at
+                # the clock the chip holds in it), frac = issue x clock / 2.4 GHz
+                # (the fraction of the 2.4 GHz int8 peak the phase runs at)
+                table = {}
+                for i, ph in enumerate(("conv12", "conv34", "conv56")):
+                    cyc_p = t[:, i + 1] - t[:, i]
+                    rt_p = r[:, i + 1] - r[:, i]
+                    okp = rt_p > 0
+                    clk_p = float(np.median(cyc_p[okp] / rt_p[okp] * 0.1))
+                    cyc_med = float(np.median(cyc_p))
+                    mfma_p = bench.MAC_PER_IMAGE[ph] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)
+                    issue = mfma_p / cyc_med
+                    table[ph] = {"us_median": float(np.median(rt_p)) / 100.0,
+                                 "gop": 2.0 * bench.MAC_PER_IMAGE[ph] * B / 1e9,
+                                 "cycles_median": cyc_med, "mfma_cycles_per_simd": mfma_p,
+                                 "clock_ghz": clk_p, "mfma_issue_at_clock": issue,
+                                 "frac_at_2p4": issue * clk_p / 2.4}
+                rec["phase_table"] = table
         out["kernels"][n] = rec
     print(json.dumps(out))
     for n, r in out["kernels"].items():
@@ -138,6 +159,10 @@ def main():
                   f"{r['frac_at_2p4']:.3f}, MFMA issue at the held clock {r['mfma_issue_at_clock']:.3f}, "
                   f"WG {r['wg_cycles_median']:.0f} cyc vs {r['wg_mfma_cycles_per_simd']:.0f} MFMA cyc/SIMD",
                   file=sys.stderr)
+        for ph, t in r.get("phase_table", {}).items():
+            print(f"#   {ph}: {t['us_median']:.1f} us, {t['cycles_median']:.0f} cyc vs {t['mfma_cycles_per_simd']:.0f} "
+                  f"MFMA cyc/SIMD, clock {t['clock_ghz']:.3f} GHz, issue {t['mfma_issue_at_clock']:.3f}, "
+                  f"frac@2.4 {t['frac_at_2p4']:.3f}", file=sys.stderr)
 
 
 if __name__ == "__main__":
