@@ -73,7 +73,7 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "conv1_6": 3 * 32 * 32 * 4 + 4 * 4 * 256 + 2 * (16 * 16 * 64 + 8 * 8 * 128)}
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
-KERNEL_SYMBOLS = {"conv1_6": ("convnet_convs_kernel", "convnet_convs_sm_kernel"),
+KERNEL_SYMBOLS = {"conv1_6": ("convnet_convs16_kernel", "convnet_convs_kernel", "convnet_convs_sm_kernel"),
                   "conv12": ("conv12p_kernel",),
                   # (the persistent wave-specialised kernel from two images per CU
                   # (four for conv5+6), the per-tile pair kernels below)
