@@ -142,6 +142,8 @@ def main():
                     okp = rt_p > 0
                     clk_p = float(np.median(cyc_p[okp] / rt_p[okp] * 0.1))
                     cyc_med = float(np.median(cyc_p))
+                    if cyc_med <= 0:   # a phase this launch does not run (a separate launch)
+                        continue
                     mfma_p = bench.MAC_PER_IMAGE[ph] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)
                     issue = mfma_p / cyc_med
                     table[ph] = {"us_median": float(np.median(rt_p)) / 100.0,
