@@ -60,6 +60,11 @@
 #ifndef QCN_M16
 #define QCN_M16 1
 #endif
+// diagnostic: s_setprio of the conv B role (waves 4-7, the second-dispatched
+// half) in the 16x16 pair phases; 0 leaves both roles at priority 0
+#ifndef QCN_WS16_BPRIO
+#define QCN_WS16_BPRIO 0
+#endif
 
 namespace qcn {
 
@@ -1906,6 +1911,7 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
       lds_barrier();
     }
   } else {
+    if (QCN_WS16_BPRIO) __builtin_amdgcn_s_setprio(QCN_WS16_BPRIO);
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
       if constexpr (!P::DOUBLE_A) lds_barrier();
@@ -1932,6 +1938,9 @@ void convpair_ws16_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, con
 
 // The headline's patch layouts for the 16x16 reads (tools/lds_banks.py)
 using W16A3 = ConvCfg<64, 128, 16, false, 2, 32, 0, 0, false>;
+// (conv4 on its r04 layout — 2-way conflicted 16x16 B reads — would leave
+// room for a double conv3 patch; measured 0.6 % slower,
+// profiles/r05_diag_w16b4_double_a_ab.txt)
 using W16B4 = ConvCfg<128, 128, 16, true, 2, 32, 64, 0, true>;
 using W16A5 = ConvCfg<128, 256, 8, false, 1, 32, 192, 0, false>;
 using W16B6 = ConvCfg<256, 256, 8, true, 1, 32, 0, 0, true>;
