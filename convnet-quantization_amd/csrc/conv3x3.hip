@@ -70,7 +70,14 @@ namespace qcn {
 
 // conv12 producer waves' issue priority (swept: 1-3 within noise, 2 best;
 // 0 is ~20 % slower, profiles/r01_diag_conv12_prio_sweep_v16.txt)
-constexpr int kProdPrio = 2;
+#ifndef QCN_PROD_PRIO
+#define QCN_PROD_PRIO 2
+#endif
+constexpr int kProdPrio = QCN_PROD_PRIO;
+// diagnostic: the conv12 consumer's priority during its epilogue (0: unchanged)
+#ifndef QCN_C2_EPI_PRIO
+#define QCN_C2_EPI_PRIO 0
+#endif
 
 // Patch layout knobs (chosen per layer by an offline bank-conflict search so
 // that every ds_read_b128 of an MFMA operand is conflict-free):
@@ -2141,6 +2148,27 @@ QCN_DEV void conv_mainloop_res(const uint8_t* patch, const uint8_t* wres,
   }
 }
 
+// Diagnostic builds only (tools/clock: -DQCN_C12_STAMP): s_memtime of lane 0
+// of waves 0 (consumer), 4 and 5 (producer) at the top of every tile
+// iteration, before its barrier and after conv2's main loop, plain vector
+// stores.  Not in the product.
+#ifdef QCN_C12_STAMP
+__device__ unsigned long long g_c12_stamp[4096][3][12][3];
+QCN_DEV void c12_stamp(int j, int k) {
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int w = threadIdx.x >> 6;
+  const int s = w == 0 ? 0 : (w == 4 ? 1 : (w == 5 ? 2 : -1));
+  if (s >= 0 && lane == 0 && blockIdx.x < 4096 && j < 12) {
+    volatile unsigned long long* d = &g_c12_stamp[blockIdx.x][s][j][k];
+    *d = t + lane;
+  }
+}
+#define C12_STAMP(j, k) c12_stamp(j, k)
+#else
+#define C12_STAMP(j, k)
+#endif
+
 // Images t0, t0 + ts, ... (T / 2 of them, each as its top then its bottom
 // half-image tile) through the producer/consumer pipeline.  512 threads, LDS
 // layout Conv12P.
@@ -2473,6 +2501,8 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     v16i acc[2][4];
     conv_mainloop_res<C>(pb, lds + L::OFF_W, reinterpret_cast<const int*>(lds + L::OFF_CORR2),
                          wave, ln, acc);
+    C12_STAMP(((t >> 1) - t0) / ts * 2 + (t & 1) + 1, 2);
+    if constexpr (QCN_C2_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(QCN_C2_EPI_PRIO);
     const int n = t >> 1, h = t & 1;
     const float* ek2 = reinterpret_cast<const float*>(lds + L::OFF_EPI2);
     uint8_t* dst = y + ((long)n * 256 + h * 128 + wave * 32 + l32) * 64;
@@ -2482,6 +2512,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     for (int i = 0; i < 2; ++i)
       epilogue_tile_kf<4, false, false, true>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi,
                                               dst, wbase, woff);
+    if constexpr (QCN_C2_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(0);
   };
 
   if (producer && T > 0) stage_load(tile_of(0));
@@ -2499,6 +2530,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
   }
   constexpr bool SPLIT0 = true;
   for (int j = 0; j <= T; ++j) {
+    C12_STAMP(j, 0);
     if (producer) {
       if (j + 1 < T) stage_load(tile_of(j + 1));
       if (j < T) {
@@ -2514,6 +2546,7 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
       conv1_tile(tile_of(0), in8_0, patch0, nullptr, wave, 8);
       __builtin_amdgcn_s_setprio(0);
     }
+    C12_STAMP(j, 1);
     __syncthreads();
   }
 }

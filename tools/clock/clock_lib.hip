@@ -16,6 +16,8 @@
 #define QCN_PIPE34_STAMP 1
 // and the one-launch conv1..conv6 kernels' per-phase stamps (g_c16_stamp)
 #define QCN_CONVNET_STAMP 1
+// and conv12p's per-tile-iteration stamps (g_c12_stamp)
+#define QCN_C12_STAMP 1
 #define qcn_conv3x3_pair_u8s8 qcn_conv3x3_pair_u8s8__product
 #define qcn_conv12_fused_f32_nchw qcn_conv12_fused_f32_nchw__product
 #include "conv3x3.hip"
@@ -211,6 +213,14 @@ int qcn_clock_read_c16(unsigned long long* host, int n) {
   if (n <= 0 || n > 4096 || !host) return QCN_ERR_ARG;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_c16_stamp), (size_t)n * 64, 0, hipMemcpyDeviceToHost) ==
                  hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
+// conv12p's per-iteration stamps of the last launch: [wg][consumer w0, producer
+// w4, producer w5][iteration 0..11][top, before barrier, after conv2's main loop] (s_memtime).
+int qcn_clock_read_c12(unsigned long long* host, int n) {
+  if (n <= 0 || n > 4096 || !host) return QCN_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_c12_stamp), (size_t)n * 3 * 12 * 3 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
 // Copy kind's stamps of the last launch ([wg][t0, t1, r0, r1], n workgroups) to host.

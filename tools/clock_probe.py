@@ -152,6 +152,27 @@ def main():
                                  "clock_ghz": clk_p, "mfma_issue_at_clock": issue,
                                  "frac_at_2p4": issue * clk_p / 2.4}
                 rec["phase_table"] = table
+                if hasattr(lib, "qcn_clock_read_c12"):   # conv12p per-iteration stamps
+                    f12 = lib.qcn_clock_read_c12
+                    f12.restype, f12.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+                    b12 = np.zeros((g, 3, 12, 3), np.uint64)
+                    _lib.check(f12(b12.ctypes.data, g), "qcn_clock_read_c12")
+                    s = b12.astype(np.float64)
+                    T = int(round(2 * img_per_wg))   # tiles of the full workgroups
+                    full = s[:, 0, T, 1] > 0
+                    s = s[full]
+                    it = {}
+                    for j in range(T + 1):
+                        top = s[:, 0, j, 0]
+                        nxt = s[:, 0, j + 1, 0] if j < T else s[:, 0, j, 1]
+                        it[str(j)] = {
+                            "iter_cycles": float(np.median(nxt - top)),
+                            "consumer_busy": float(np.median(s[:, 0, j, 1] - s[:, 0, j, 0])),
+                            "consumer_mainloop": float(np.median(s[:, 0, j, 2] - s[:, 0, j, 0])) if j > 0 else 0.0,
+                            "producer_w4_busy": float(np.median(s[:, 1, j, 1] - s[:, 1, j, 0])),
+                            "producer_w5_busy": float(np.median(s[:, 2, j, 1] - s[:, 2, j, 0])),
+                        }
+                    rec["conv12_iterations"] = {"workgroups": int(full.sum()), "tiles": T, "per_iteration": it}
         out["kernels"][n] = rec
     print(json.dumps(out))
     for n, r in out["kernels"].items():
@@ -161,6 +182,11 @@ def main():
                   f"{r['frac_at_2p4']:.3f}, MFMA issue at the held clock {r['mfma_issue_at_clock']:.3f}, "
                   f"WG {r['wg_cycles_median']:.0f} cyc vs {r['wg_mfma_cycles_per_simd']:.0f} MFMA cyc/SIMD",
                   file=sys.stderr)
+        ci = r.get("conv12_iterations")
+        if ci:
+            for j, v in ci["per_iteration"].items():
+                print(f"#   conv12 iter {j}: {v['iter_cycles']:.0f} cyc, consumer busy {v['consumer_busy']:.0f} (main loop {v['consumer_mainloop']:.0f}), "
+                      f"producer w4 {v['producer_w4_busy']:.0f}, w5 {v['producer_w5_busy']:.0f}", file=sys.stderr)
         for ph, t in r.get("phase_table", {}).items():
             print(f"#   {ph}: {t['us_median']:.1f} us, {t['cycles_median']:.0f} cyc vs {t['mfma_cycles_per_simd']:.0f} "
                   f"MFMA cyc/SIMD, clock {t['clock_ghz']:.3f} GHz, issue {t['mfma_issue_at_clock']:.3f}, "
