@@ -1628,8 +1628,14 @@ QCN_DEV void pipe_job16(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_
     return *reinterpret_cast<const v4i*>(patch + lb + X::jofs(j) + PatchAddr<C>::delta(tap, j) + cb * 64);
   };
   auto issue = [&](wt_rsrc_t r, int s, int slot) {
+#if defined(QCN_EXP_WA_SAME)   // diagnostic probe only (wrong results): every step loads step 0's chunk
+    s = 0;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+#if defined(QCN_EXP_WA_NONE)   // diagnostic probe only (wrong results): no weight loads after the first
+      if (s != 0) { ga[slot][i] = ga[slot ^ 1][i]; continue; }
+#endif
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, s * C::WBUF + i * 1024, 0);
       ga[slot][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
     }
