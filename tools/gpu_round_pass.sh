@@ -9,6 +9,9 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+( while sleep 50; do echo "alive $(date +%T)"; done ) &
+HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
