@@ -80,6 +80,14 @@ struct GemmArgs {
   // streaming 1x1 kernel: 32-pixel strips, chunks of `per` strips, `cg`
   // channel groups of NW x 32 output channels
   int nstrip, nchunk, per, cg;
+  // fused next-block reduce (CR > 0): 1x1 conv of the joined output y (its
+  // input zero point z_o), k-major weights [K/32][CR][32], FBGEMM requant
+  // (u2, v2, mult2, corr2, zp2, lo2) into y2 [pixel][CR]
+  const int8_t* w2;
+  const float *u2, *v2, *mult2;
+  const int* corr2;
+  int zp2, lo2;
+  uint8_t* y2;
 };
 
 template <int BN, int BM_ = 256>
@@ -496,6 +504,9 @@ QCN_DEV v4i asm_bload(v4i rs, int voff) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rs) : "memory");
   return r;
 }
+QCN_DEV void asm_bstore4(v4i rs, int voff, uint32_t d) {
+  asm volatile("buffer_store_dword %0, %1, %2, 0 offen" :: "v"(d), "v"(voff), "s"(rs) : "memory");
+}
 QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
   // s_nop: a VALU write of a >8-byte store's data VGPR right behind the store
   // needs a wait state (the hazard recognizer does not see inside asm)
@@ -542,8 +553,9 @@ QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
 // B(j) x NB, I(j) for j < P; step t issues S(t), B(t+P) x NB, I(t+P) after its
 // waits.  BL = false waits at the head of step t for B(t), I(t); BL = true
 // waits before step t's barrier for B(t+1), I(t) (t = -1: the prologue's wait
-// for B(0)).  Returns the number of younger operations that may stay in flight.
-constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t) {
+// for B(0)).  NS: stores per step (1, or 1 + the fused reduce's).  Returns the
+// number of younger operations that may stay in flight.
+constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t, int NS = 1) {
   int pos = 0, last = -1;
   auto issue_b = [&](int strip) {
     for (int i = 0; i < NB; ++i) {
@@ -557,13 +569,15 @@ constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t) {
     ++pos;
   };
   for (int j = 0; j < P; ++j) { issue_b(j); issue_i(j); }
-  for (int u = 0; u < t; ++u) { ++pos; issue_b(u + P); issue_i(u + P); }
+  for (int u = 0; u < t; ++u) { pos += NS; issue_b(u + P); issue_i(u + P); }
   return pos - 1 - last;
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false>
-__global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_kernel(GemmArgs a) {
+template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false, int CR = 0>
+__global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void conv1x1_stream_kernel(GemmArgs a) {
   static_assert(!S2 || BL, "stride 2 reads its rows through the LDS ring");
+  static_assert(CR == 0 || (RESID && K == 64 && NW == 8 && !BL && (CR == 64 || CR == 128)),
+                "the fused reduce follows a 64 -> 256 expand + join (one workgroup holds a strip's 256 channels)");
   constexpr int KC = K / 32;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -610,6 +624,41 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   const v2f jav = {a.s3, a.s3}, jbv = {a.s_r, a.s_r}, jcv = {a.inv_o, a.inv_o};
   const int lastp = (int)(a.npix - 1);   // npix < 2^31 - 256 (checked at the ABI)
 
+  // Fused reduce (CR > 0): the next bottleneck's 1x1 conv (K = 256 -> CR) on
+  // the strip's joined bytes, which never leave the chip for it.  The joined
+  // 32 x 256 tile goes to LDS (q ^ 0x80, pixel stride 288 B: 16 B x (2 mod 4),
+  // conflict-free for the 16x16 B reads); the (CR / 16) x 2 jobs of 16 couts x
+  // 16 pixels on v_mfma_i32_16x16x64_i8 spread over the 8 waves (NJ per wave),
+  // their A fragments (4 K-steps x 16 B per lane) and requant constants
+  // resident in registers.  Lane (p, g) of a job holds couts 4g .. 4g + 3 of
+  // its pixel p: one dword store per lane and job.
+  constexpr int NJ = CR > 0 ? CR / 64 : 1, RS2 = 288;
+  const int p16 = lane & 15, g16 = lane >> 4;
+  v4i wr2[NJ][4];
+  float4 ru[NJ], rv[NJ], rm[NJ];
+  int4 rc[NJ];
+  if constexpr (CR > 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int job = wave + 8 * j, c16 = job % (CR / 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        wr2[j][s] = *reinterpret_cast<const v4i*>(a.w2 + ((long)(2 * s + (g16 >> 1)) * CR + c16 * 16 + p16) * 32 +
+                                                  16 * (g16 & 1));
+      const int co = c16 * 16 + 4 * g16;
+      ru[j] = *reinterpret_cast<const float4*>(a.u2 + co);
+      rv[j] = *reinterpret_cast<const float4*>(a.v2 + co);
+      rm[j] = *reinterpret_cast<const float4*>(a.mult2 + co);
+      rc[j] = *reinterpret_cast<const int4*>(a.corr2 + co);
+      asm volatile("" :: "v"(wr2[j][0]), "v"(wr2[j][1]), "v"(wr2[j][2]), "v"(wr2[j][3]));
+      asm volatile("" :: "v"(ru[j].x), "v"(ru[j].y), "v"(ru[j].z), "v"(ru[j].w), "v"(rv[j].x), "v"(rv[j].y),
+                   "v"(rv[j].z), "v"(rv[j].w));
+      asm volatile("" :: "v"(rm[j].x), "v"(rm[j].y), "v"(rm[j].z), "v"(rm[j].w), "v"(rc[j].x), "v"(rc[j].y),
+                   "v"(rc[j].z), "v"(rc[j].w));
+    }
+  }
+  const float zp2f = (float)a.zp2, lo2f = (float)a.lo2;
+
   // 32-bit buffer offsets (activations, identity and output are < 2 GiB:
   // checked at launch).  Every memory operation is unconditional: pixel rows
   // past the end (and strips past s1) are clamped to the last pixel, whose
@@ -619,6 +668,7 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   // compiler's own bookkeeping falls back to vmcnt(0) at the loop head, which
   // drains the prefetch every round.
   const v4i xr = buf_rsrc(a.x), rr = buf_rsrc(a.r), yr = buf_rsrc(a.y);
+  const v4i y2r = buf_rsrc(CR > 0 ? a.y2 : a.y);
   auto pix = [&](int st, int row) {
     st = st < s1 ? st : s1 - 1;
     const int p = st * 32 + row;
@@ -634,6 +684,7 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   constexpr int RING = BL ? P * 32 * K + (NDMA * NW > KC ? 1024 : 0) : 16;
   static_assert(!BL || NDMA * NW == KC || NDMA == 1, "pieces split evenly, or one per wave");
   __shared__ __attribute__((aligned(16))) uint8_t tile[2][32 * RS];
+  __shared__ __attribute__((aligned(16))) uint8_t tile2[CR > 0 ? 2 : 1][CR > 0 ? 32 * RS2 : 16];
   __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
   const int rrow = wave * RPW + lane / LPR, rcol = (lane % LPR) * 16;
   const int cb0 = cgi * ROWB;
@@ -674,7 +725,7 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   // wait at step t (slot q): the asm ties the slot's registers, so no use of
   // them moves above it
   auto wait_vm = [&](auto tc, int q) {
-    constexpr int N = stream_vmcnt(P, NB, RESID, BL, decltype(tc)::value);
+    constexpr int N = stream_vmcnt(P, NB, RESID, BL, decltype(tc)::value, CR > 0 ? 1 + NJ : 1);
     if constexpr (!BL) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) asm volatile("" : "+v"(bq[q][kc]));
@@ -777,7 +828,43 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
         w[g] = o;
       }
     }
+    uint32_t rd[NJ];   // the fused reduce's requantized dwords
+    if constexpr (CR > 0) {
+      uint8_t* t2 = tile2[st & 1];
+      *reinterpret_cast<v4i*>(t2 + rrow * RS2 + rcol) =
+          (v4i){(int)(w[0] ^ 0x80808080u), (int)(w[1] ^ 0x80808080u), (int)(w[2] ^ 0x80808080u),
+                (int)(w[3] ^ 0x80808080u)};
+      // every row of the strip is in tile2; tile2[st & 1]'s previous readers
+      // (strip st - 2) passed this strip's first barrier after their reads
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int job = wave + 8 * j, pb = job / (CR / 16);
+        const uint8_t* bp = t2 + (pb * 16 + p16) * RS2 + 16 * g16;
+        v4i acc2 = (v4i){rc[j].x, rc[j].y, rc[j].z, rc[j].w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(wr2[j][s], *reinterpret_cast<const v4i*>(bp + 64 * s), acc2,
+                                                       0, 0, 0);
+        const float uu[4] = {ru[j].x, ru[j].y, ru[j].z, ru[j].w}, vv[4] = {rv[j].x, rv[j].y, rv[j].z, rv[j].w};
+        const float mm[4] = {rm[j].x, rm[j].y, rm[j].z, rm[j].w};
+        uint32_t wd = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float f = __builtin_fmaf(uu[e], vv[e], (float)acc2[e]) * mm[e];
+          wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(f) + zp2f, lo2f, 255.0f), e, wd);
+        }
+        rd[j] = wd;
+      }
+    }
     asm_bstore(yr, pix(st, rrow) * cout + cb0 + rcol, (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]});
+    if constexpr (CR > 0) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int job = wave + 8 * j, c16 = job % (CR / 16), pb = job / (CR / 16);
+        asm_bstore4(y2r, pix(st, pb * 16 + p16) * CR + c16 * 16 + 4 * g16, rd[j]);
+      }
+    }
     load(q, st + P);   // refill the slot
   };
 #pragma unroll
@@ -803,9 +890,9 @@ __global__ __launch_bounds__(NW * 64, (K == 64 ? 3 : 2)) void conv1x1_stream_ker
   }
 }
 
-template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false>
+template <int K, int NW, bool RESID, int P, int RQ, int ZO, bool BL, bool S2 = false, int CR = 0>
 int launch_stream(GemmArgs& a, hipStream_t st) {
-  const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL, S2>;
+  const auto kern = conv1x1_stream_kernel<K, NW, RESID, P, RQ, ZO, BL, S2, CR>;
   static int occ_dev[QCN_MAX_DEV] = {};
   const int d = qcn_current_device(), ncu = qcn_cu_count();
   if (d < 0 || ncu <= 0) return QCN_ERR_HIP;
@@ -919,6 +1006,26 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
                                       : launch_stream<K, NW, false, P, 1, true, BL>(a, st);
     return launch_stream<K, NW, false, P, 2, true, BL>(a, st);
   }
+}
+
+// The layer-1 expand + join (K = 64 -> 256) with the next block's reduce
+// (256 -> CR) fused: 8 waves per workgroup so one holds a strip's 256 joined
+// channels; the join's forms as stream_modes.
+template <int CR>
+int join_reduce_modes(GemmArgs& a, hipStream_t st) {
+  float j[3];
+  if (QCN_JOIN_AFF && a.z_o == 0 && join_affine_solve(a, j)) {
+    GemmArgs b = a;
+    b.s3 = j[0]; b.s_r = j[1]; b.inv_o = j[2];
+    return a.zp_y == 0 ? launch_stream<64, 8, true, 4, 0, 2, false, false, CR>(b, st)
+                       : launch_stream<64, 8, true, 4, 1, 2, false, false, CR>(b, st);
+  }
+  const int zo = a.z_o == 0 ? 1 : 0;
+  if (a.zp_y == 0)
+    return zo ? launch_stream<64, 8, true, 4, 0, 1, false, false, CR>(a, st)
+              : launch_stream<64, 8, true, 4, 0, 0, false, false, CR>(a, st);
+  return zo ? launch_stream<64, 8, true, 4, 1, 1, false, false, CR>(a, st)
+            : launch_stream<64, 8, true, 4, 1, 0, false, false, CR>(a, st);
 }
 
 // K in {64, 128, 256, 512}; Cout % 128 == 0 (4 waves per workgroup), or
@@ -1164,6 +1271,39 @@ extern "C" int qcn_join_affine(float y_scale, int y_zp, float r_scale, int r_zp,
   qcn::GemmArgs a{};
   a.s3 = y_scale; a.zp_y = y_zp; a.s_r = r_scale; a.z_r = r_zp; a.inv_o = 1.0f / out_scale;
   return qcn::join_affine_solve(a, out) ? 1 : 0;
+}
+
+extern "C" int qcn_conv1x1_join_reduce_u8s8_nhwc(
+    const uint8_t* x, int nimg, int h, int w, int cin, int x_zp, const int8_t* w_packed, int cout,
+    const float* u, const float* v, const float* mult, const int32_t* corr, int y_zp, const uint8_t* resid,
+    float y_scale, float r_scale, int r_zp, float out_scale, int out_zp, uint8_t* y, const int8_t* w2_packed,
+    int cout2, const float* u2, const float* v2, const float* mult2, const int32_t* corr2, int y2_zp, int relu2,
+    uint8_t* y2, void* stream) {
+  if (!x || !w_packed || !u || !v || !mult || !corr || !resid || !y || !w2_packed || !u2 || !v2 || !mult2 ||
+      !corr2 || !y2)
+    return QCN_ERR_ARG;
+  if (nimg <= 0 || h <= 0 || w <= 0 || x_zp < 0 || x_zp > 255 || y_zp < 0 || y_zp > 255 || r_zp < 0 ||
+      r_zp > 255 || out_zp < 0 || out_zp > 255 || y2_zp < 0 || y2_zp > 255 || !(y_scale > 0.f) ||
+      !(r_scale > 0.f) || !(out_scale > 0.f))
+    return QCN_ERR_ARG;
+  if (cin != 64 || cout != 256 || (cout2 != 64 && cout2 != 128)) return QCN_ERR_UNSUPPORTED;
+  qcn::GemmArgs a{};
+  a.x = x; a.w = w_packed;
+  a.n = nimg; a.h = h; a.w_ = w; a.cin = cin; a.oh = h; a.ow = w; a.cout = cout;
+  a.kh = 1; a.kw = 1; a.sy = 1; a.sx = 1; a.py = 0; a.px = 0;
+  a.x_zp = x_zp;
+  a.npix = (long)nimg * h * w;
+  a.kcs = cin / 32;
+  a.u = u; a.v = v; a.mult = mult; a.corr = corr;
+  a.zp_y = y_zp; a.lo = 0;
+  a.r = resid; a.s3 = y_scale; a.s_r = r_scale; a.inv_o = 1.0f / out_scale;
+  a.z_r = r_zp; a.z_o = out_zp; a.y = y;
+  a.w2 = w2_packed; a.u2 = u2; a.v2 = v2; a.mult2 = mult2; a.corr2 = corr2;
+  a.zp2 = y2_zp; a.lo2 = relu2 ? y2_zp : 0; a.y2 = y2;
+  // 32-bit buffer offsets and pixel indices in the kernel
+  if (a.npix * (long)cout >= (1L << 31) - 4096) return QCN_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  return cout2 == 64 ? qcn::join_reduce_modes<64>(a, st) : qcn::join_reduce_modes<128>(a, st);
 }
 
 extern "C" int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,

@@ -91,6 +91,9 @@ SIGNATURES = {
     "qcn_conv_gemm_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32,
                                       i32, vp, vp, vp, vp, i32, i32, vp, f32, f32, i32, f32, i32,
                                       vp, vp]),
+    "qcn_conv1x1_join_reduce_u8s8_nhwc": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp,
+                                                f32, f32, i32, f32, i32, vp, vp, i32, vp, vp, vp, vp, i32,
+                                                i32, vp, vp]),
     "qcn_add_relu_u8": (i32, [vp, f32, i32, vp, f32, i32, i64, f32, i32, i32, vp, vp]),
     "qcn_maxpool3x3s2_u8_nhwc": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "qcn_stem_pack_f32_nchw": (i32, [vp, i32, i32, i32, f32, i32, vp, vp]),

@@ -441,6 +441,34 @@ def conv(x, x_zp, layer, out=None, resid=None, impl=None):
     return out
 
 
+def conv_join_reduce(x, x_zp, layer, resid, nxt, out=None, out2=None):
+    """``conv(x, x_zp, layer, resid=resid)`` (the 64 -> 256 expand + residual
+    join) and ``conv(result, resid[4], nxt)`` (the next block's 1x1 reduce,
+    256 -> 64 or 128) in one launch (qcn_conv1x1_join_reduce_u8s8_nhwc);
+    returns (joined, reduced), bit-identical to the two launches.  None when
+    the library declines the shape (QCN_ERR_UNSUPPORTED)."""
+    _need(x, torch.uint8, "conv_join_reduce.x")
+    n, h, w, cin = x.shape
+    d, e = layer, nxt
+    r, s_r, z_r, s_o, z_o = resid
+    _need(r, torch.uint8, "conv_join_reduce.resid")
+    if out is None:
+        out = torch.empty((n, h, w, d.cout), dtype=torch.uint8, device=x.device)
+    if tuple(r.shape) != tuple(out.shape):
+        raise ValueError("residual operand shape differs from the conv output")
+    if out2 is None:
+        out2 = torch.empty((n, h, w, e.cout), dtype=torch.uint8, device=x.device)
+    rc = lib().qcn_conv1x1_join_reduce_u8s8_nhwc(
+        _ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, _ptr(d.u), _ptr(d.v), _ptr(d.mult),
+        _ptr(d.corr), int(d.z_y), _ptr(r), float(d.s_y), float(s_r), int(z_r), float(s_o), int(z_o),
+        _ptr(out), _ptr(e.w), e.cout, _ptr(e.u), _ptr(e.v), _ptr(e.mult), _ptr(e.corr), int(e.z_y),
+        int(bool(e.relu)), _ptr(out2), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return None
+    check(rc, "conv_join_reduce")
+    return out, out2
+
+
 def add_relu(a, sa, za, b, sb, zb, s_out, z_out, relu=True, out=None):
     _need(a, torch.uint8, "add.a")
     _need(b, torch.uint8, "add.b")

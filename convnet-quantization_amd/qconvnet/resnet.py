@@ -170,6 +170,9 @@ class QuantizedResNet:
         self.quantized = True
         self.host_io = False
         self._graphs = {}
+        # the layer-1 expand + join launches also run the next block's reduce
+        # conv (qcn_conv1x1_join_reduce_u8s8_nhwc); False: separate launches
+        self.fuse_reduce = True
         self._upload()
 
     def _t(self, a):
@@ -235,6 +238,15 @@ class QuantizedResNet:
                 and tuple(np.asarray(e["w"]).shape[1:]) == (3, 7, 7)
                 and tuple(e["stride"]) == (2, 2) and tuple(e["pad"]) == (3, 3)
                 and x.shape[1] == 3 and x.shape[2] == x.shape[3] and x.shape[2] in (224, 64))
+
+    @staticmethod
+    def _join_reduce_fusable(c3, c1n):
+        """c3 (+ join) and the next block's c1 in one launch: the 64 -> 256 1x1
+        expand and a 1x1 stride-1 256 -> 64 / 128 reduce (ResNet-50 layer 1 and
+        the first reduce of layer 2)."""
+        one = lambda d: (d.kh, d.kw, d.sy, d.sx, d.py, d.px) == (1, 1, 1, 1, 0, 0)
+        return (one(c3) and one(c1n) and c3.cin == 64 and c3.cout == 256 and c1n.cin == 256
+                and c1n.cout in (64, 128))
 
     def conv_layers(self):
         """Every conv launch in forward order (for MAC accounting)."""
@@ -319,6 +331,7 @@ class QuantizedResNet:
             yield
         if keep:
             inter["stem"] = q
+        pending = None   # this block's c1 output, when the previous launch fused it
         for i, (b, e) in enumerate(zip(self.blocks, sp["blocks"])):
             zx = b["c1"].z_x
             if b["ds"] is not None:   # identity first, so conv3 can consume it
@@ -328,16 +341,28 @@ class QuantizedResNet:
                 si, zi = e["ds"]["s_y"], e["ds"]["z_y"]
             else:
                 idn, si, zi = q, e["c1"]["s_x"], zx
-            y = ops.conv(q, zx, b["c1"])
-            mark("conv")
-            yield
+            if pending is not None:
+                y, pending = pending, None
+            else:
+                y = ops.conv(q, zx, b["c1"])
+                mark("conv")
+                yield
             yh = self._conv3x3_halo(y, b["c2"])
             y = yh if yh is not None else ops.conv(y, b["c2"].z_x, b["c2"])
             mark("conv")
             yield
             so, zo = e["out"]
-            # conv3 + residual join in one launch
-            q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
+            # conv3 + residual join in one launch, with the next block's reduce
+            # conv where the shapes allow (its input is this join's output)
+            nb = self.blocks[i + 1] if i + 1 < len(self.blocks) else None
+            fused = None
+            if self.fuse_reduce and nb is not None and self._join_reduce_fusable(b["c3"], nb["c1"]):
+                assert nb["c1"].z_x == int(zo), "the next reduce reads this join's output"
+                fused = ops.conv_join_reduce(y, b["c3"].z_x, b["c3"], (idn, si, zi, so, zo), nb["c1"])
+            if fused is not None:
+                q, pending = fused
+            else:
+                q = ops.conv(y, b["c3"].z_x, b["c3"], resid=(idn, si, zi, so, zo))
             mark("conv")
             yield
             if keep:

@@ -312,6 +312,21 @@ int qcn_conv_gemm_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, i
                             const float* mult, const int32_t* corr, int y_zp, int relu,
                             const uint8_t* resid, float y_scale, float r_scale, int r_zp,
                             float out_scale, int out_zp, uint8_t* y, void* stream);
+/* The bottleneck's expand + residual join (qcn_conv_gemm_u8s8_nhwc with
+ * resid, 1x1, cin 64 -> cout 256) with the NEXT block's reduce conv (1x1,
+ * stride 1, 256 -> cout2 in {64, 128}, input zero point out_zp) fused: y is
+ * the joined block output (u8 NHWC [n][h][w][256], the next identity), y2 the
+ * reduce's output [n][h][w][cout2] (FBGEMM requant with u2/v2/mult2/corr2,
+ * y2_zp, relu2).  Bit-identical to the two separate launches; replaces
+ * custom_quantization_model.py:89-101 of block i followed by :81-83 (conv1,
+ * bn1, relu) of block i + 1.  QCN_ERR_UNSUPPORTED for other shapes. */
+int qcn_conv1x1_join_reduce_u8s8_nhwc(const uint8_t* x, int nimg, int h, int w, int cin, int x_zp,
+                                      const int8_t* w_packed, int cout, const float* u, const float* v,
+                                      const float* mult, const int32_t* corr, int y_zp, const uint8_t* resid,
+                                      float y_scale, float r_scale, int r_zp, float out_scale, int out_zp,
+                                      uint8_t* y, const int8_t* w2_packed, int cout2, const float* u2,
+                                      const float* v2, const float* mult2, const int32_t* corr2, int y2_zp,
+                                      int relu2, uint8_t* y2, void* stream);
 /* Residual join (custom_quantization_model.py:94-101 then the next stage's
  * QuantStub): y = quantize(relu?(fp32(sa*(a-za)) + fp32(sb*(b-zb))), s_out, z_out). */
 int qcn_add_relu_u8(const uint8_t* a, float sa, int za, const uint8_t* b, float sb, int zb,

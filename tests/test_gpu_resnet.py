@@ -182,6 +182,56 @@ def test_conv1x1_stream_oracle(dev, shape):
 
 
 @pytest.mark.parametrize("shape", [
+    # n, h, w, expand zx, expand zy, join z_o, reduce cout, reduce zy, reduce relu, per_channel
+    (3, 7, 9, 5, 30, 0, 64, 0, True, True),        # 189 pixels: ragged last strip
+    (2, 56, 56, 0, 0, 23, 64, 0, True, True),      # the layer-1 shape; z_o != 0
+    (1, 13, 11, 77, 9, 0, 128, 12, True, False),   # the layer-2 first reduce (cout 128), ReLU floor 12
+    (2, 5, 5, 130, 2, 7, 128, 40, False, True),    # no ReLU: general clamp
+    (1, 1, 1, 9, 3, 0, 64, 0, True, True),         # one pixel
+])
+def test_conv1x1_join_reduce_oracle(dev, shape):
+    """The expand + join launch with the next block's reduce conv fused
+    (qcn_conv1x1_join_reduce_u8s8_nhwc) against the oracle's conv -> add_relu_q
+    -> conv, and against the two separate launches."""
+    from qconvnet import ops
+    n, h, w, zx, zy, zo, cr, zr, relur, pc = shape
+    rng = np.random.default_rng(hash(shape) & 0xffff)
+    qx = rng.integers(0, 256, (n, h, w, 64)).astype(np.uint8)
+
+    def wts(cout, cin):
+        wf = (rng.standard_normal((cout, cin, 1, 1)) * 0.05).astype(F32)
+        s_w = qref.qparams_symmetric(wf.reshape(cout, -1).min(1), wf.reshape(cout, -1).max(1))[0] if pc \
+            else qref.qparams_symmetric(wf.min(), wf.max())[0]
+        return qref.quantize_weight(wf, s_w), s_w, (rng.standard_normal(cout) * 0.3).astype(F32)
+
+    w3, sw3, b3 = wts(256, 64)
+    w1, sw1, b1 = wts(cr, 256)
+    s_x, s_y, s_o, s_y2 = F32(0.02), F32(0.15), F32(0.05), F32(0.4)
+    d3 = _layer(dev, w3, s_x, sw3, s_y, b3, zx, zy, False, (1, 1), (0, 0))
+    d3.s_y = s_y
+    d1 = _layer(dev, w1, s_o, sw1, s_y2, b1, zo, zr, relur, (1, 1), (0, 0))
+    r = rng.integers(0, 256, (n, h, w, 256)).astype(np.uint8)
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    resid = (T(r), F32(0.03), 17, s_o, zo)
+    got = ops.conv_join_reduce(T(qx), zx, d3, resid, d1)
+    assert got is not None, "the library declined a supported shape"
+    q, y2 = (t.cpu().numpy() for t in got)
+    u, v, mult = qref.requant_constants(s_x, sw3, s_y, b3)
+    y3 = qref.conv_q(qx, zx, w3, u, v, mult, zy, False, (1, 1), (0, 0))
+    qj = qref.add_relu_q(y3, s_y, zy, r, F32(0.03), 17, s_o, zo)
+    u1, v1, m1 = qref.requant_constants(s_o, sw1, s_y2, b1)
+    ref2 = qref.conv_q(qj, zo, w1, u1, v1, m1, zr, relur, (1, 1), (0, 0))
+    assert np.array_equal(q, qj)
+    assert np.array_equal(y2, ref2)
+    if n * h * w > 1:
+        assert len(np.unique(ref2)) > 8, "degenerate case"
+    # the two launches it replaces
+    q_sep = ops.conv(T(qx), zx, d3, resid=resid)
+    y2_sep = ops.conv(q_sep, zo, d1)
+    assert np.array_equal(q_sep.cpu().numpy(), q) and np.array_equal(y2_sep.cpu().numpy(), y2)
+
+
+@pytest.mark.parametrize("shape", [
     # n, h, w, cin, cout, zx, zy, per_channel
     (3, 28, 28, 256, 512, 7, 90, True),
     (2, 14, 14, 512, 1024, 0, 0, True),
@@ -362,6 +412,14 @@ def test_resnet_run_streams_equals_run(dev, nsplit):
     for _ in range(2):   # second pass: side streams reused
         out = qm.run_streams(x, nsplit)
         assert torch.equal(out, ref)
+    # the layer-1 join with layer 2's first reduce fused (the default) equals
+    # the separate launches
+    assert qm.fuse_reduce
+    qm.fuse_reduce = False
+    try:
+        assert torch.equal(qm.run(x), ref)
+    finally:
+        qm.fuse_reduce = True
     torch.cuda.synchronize()
 
 
