@@ -504,9 +504,6 @@ QCN_DEV v4i asm_bload(v4i rs, int voff) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rs) : "memory");
   return r;
 }
-QCN_DEV void asm_bstore4(v4i rs, int voff, uint32_t d) {
-  asm volatile("buffer_store_dword %0, %1, %2, 0 offen" :: "v"(d), "v"(voff), "s"(rs) : "memory");
-}
 QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
   // s_nop: a VALU write of a >8-byte store's data VGPR right behind the store
   // needs a wait state (the hazard recognizer does not see inside asm)
@@ -553,9 +550,12 @@ QCN_DEV void asm_bstore(v4i rs, int voff, v4i d) {
 // B(j) x NB, I(j) for j < P; step t issues S(t), B(t+P) x NB, I(t+P) after its
 // waits.  BL = false waits at the head of step t for B(t), I(t); BL = true
 // waits before step t's barrier for B(t+1), I(t) (t = -1: the prologue's wait
-// for B(0)).  NS: stores per step (1, or 1 + the fused reduce's).  Returns the
-// number of younger operations that may stay in flight.
-constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t, int NS = 1) {
+// for B(0)).  NS: stores per step (2 with the fused reduce: its previous
+// strip's output is stored after the step's first barrier), NS0 at a chunk's
+// first step.  The steady-state bound (t = P) is modelled on a first round, so
+// with NS0 < NS it is one op conservative.  Returns the number of younger
+// operations that may stay in flight.
+constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t, int NS = 1, int NS0 = 1) {
   int pos = 0, last = -1;
   auto issue_b = [&](int strip) {
     for (int i = 0; i < NB; ++i) {
@@ -569,7 +569,7 @@ constexpr int stream_vmcnt(int P, int NB, bool RESID, bool BL, int t, int NS = 1
     ++pos;
   };
   for (int j = 0; j < P; ++j) { issue_b(j); issue_i(j); }
-  for (int u = 0; u < t; ++u) { pos += NS; issue_b(u + P); issue_i(u + P); }
+  for (int u = 0; u < t; ++u) { pos += u == 0 ? NS0 : NS; issue_b(u + P); issue_i(u + P); }
   return pos - 1 - last;
 }
 
@@ -631,7 +631,9 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
   // 16 pixels on v_mfma_i32_16x16x64_i8 spread over the 8 waves (NJ per wave),
   // their A fragments (4 K-steps x 16 B per lane) and requant constants
   // resident in registers.  Lane (p, g) of a job holds couts 4g .. 4g + 3 of
-  // its pixel p: one dword store per lane and job.
+  // its pixel p: one dword per lane and job into an LDS [32][CR] tile, which
+  // the next strip stores as whole 16-B row pieces after its first barrier
+  // (dword stores of the MFMA layout cost the CR = 128 form ~0.1 ms).
   constexpr int NJ = CR > 0 ? CR / 64 : 1, RS2 = 288;
   const int p16 = lane & 15, g16 = lane >> 4;
   v4i wr2[NJ][4];
@@ -685,6 +687,20 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
   static_assert(!BL || NDMA * NW == KC || NDMA == 1, "pieces split evenly, or one per wave");
   __shared__ __attribute__((aligned(16))) uint8_t tile[2][32 * RS];
   __shared__ __attribute__((aligned(16))) uint8_t tile2[CR > 0 ? 2 : 1][CR > 0 ? 32 * RS2 : 16];
+  // the reduce's strip output [32][CR] (row stride RS3), stored as whole 16-B
+  // row pieces in the NEXT strip, after its first barrier
+  constexpr int RS3 = CR + 16;
+  __shared__ __attribute__((aligned(16))) uint8_t tile3[CR > 0 ? 2 : 1][CR > 0 ? 32 * RS3 : 16];
+  int last_st = 0;
+  auto store_reduced = [&](int sp) {   // strip sp's reduce output: CR / 4 pieces per wave
+    if constexpr (CR > 0) {
+      if (lane < CR / 4) {
+        const int piece = wave * (CR / 4) + lane, row = piece / (CR / 16), c = piece % (CR / 16);
+        const v4i v = *reinterpret_cast<const v4i*>(tile3[sp & 1] + row * RS3 + 16 * c);
+        asm_bstore(y2r, pix(sp, row) * CR + 16 * c, v);
+      }
+    }
+  };
   __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
   const int rrow = wave * RPW + lane / LPR, rcol = (lane % LPR) * 16;
   const int cb0 = cgi * ROWB;
@@ -725,7 +741,7 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
   // wait at step t (slot q): the asm ties the slot's registers, so no use of
   // them moves above it
   auto wait_vm = [&](auto tc, int q) {
-    constexpr int N = stream_vmcnt(P, NB, RESID, BL, decltype(tc)::value, CR > 0 ? 1 + NJ : 1);
+    constexpr int N = stream_vmcnt(P, NB, RESID, BL, decltype(tc)::value, CR > 0 ? 2 : 1, 1);
     if constexpr (!BL) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) asm volatile("" : "+v"(bq[q][kc]));
@@ -795,6 +811,12 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
     // every wave's reads of strip st's); the other tile buffer's readers
     // (strip st-1) passed this barrier only after their reads
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (CR > 0) {
+      // strip st - 1's reduce output (complete in tile3: every wave wrote its
+      // part before this barrier); a chunk's first strip has none
+      if (st != s0) store_reduced(st - 1);
+      last_st = st;
+    }
     {
       const v4i yv = *reinterpret_cast<const v4i*>(tb + rrow * RS + rcol);
 #pragma unroll
@@ -828,7 +850,6 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
         w[g] = o;
       }
     }
-    uint32_t rd[NJ];   // the fused reduce's requantized dwords
     if constexpr (CR > 0) {
       uint8_t* t2 = tile2[st & 1];
       *reinterpret_cast<v4i*>(t2 + rrow * RS2 + rcol) =
@@ -854,17 +875,11 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
           const float f = __builtin_fmaf(uu[e], vv[e], (float)acc2[e]) * mm[e];
           wd = __builtin_amdgcn_cvt_pk_u8_f32(__builtin_amdgcn_fmed3f(__builtin_rintf(f) + zp2f, lo2f, 255.0f), e, wd);
         }
-        rd[j] = wd;
+        const int c16 = job % (CR / 16);
+        *reinterpret_cast<uint32_t*>(tile3[st & 1] + (pb * 16 + p16) * RS3 + c16 * 16 + 4 * g16) = wd;
       }
     }
     asm_bstore(yr, pix(st, rrow) * cout + cb0 + rcol, (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]});
-    if constexpr (CR > 0) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int job = wave + 8 * j, c16 = job % (CR / 16), pb = job / (CR / 16);
-        asm_bstore4(y2r, pix(st, pb * 16 + p16) * CR + c16 * 16 + 4 * g16, rd[j]);
-      }
-    }
     load(q, st + P);   // refill the slot
   };
 #pragma unroll
@@ -876,6 +891,10 @@ __global__ __launch_bounds__(NW * 64, (CR > 0 ? 1 : (K == 64 ? 3 : 2))) void con
   static_for<0, P>([&](auto q) { strip(q, q, s0 + q); });
   for (int s = s0 + P; s < s1; s += P) {
     static_for<0, P>([&](auto q) { strip(std::integral_constant<int, P>{}, q, s + q); });
+  }
+  if constexpr (CR > 0) {   // the last strip's reduce output
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    store_reduced(last_st);
   }
   // drain: the last refills are never consumed; keep their registers live
   // until they landed
