@@ -55,6 +55,7 @@ MAC_PER_IMAGE["conv34"] = MAC_PER_IMAGE["conv3"] + MAC_PER_IMAGE["conv4"]
 MAC_PER_IMAGE["conv56"] = MAC_PER_IMAGE["conv5"] + MAC_PER_IMAGE["conv6"]
 MAC_PER_IMAGE["net"] = sum(MAC_PER_IMAGE[f"conv{i}"] for i in range(1, 7))
 MAC_PER_IMAGE["conv1_6"] = MAC_PER_IMAGE["net"]   # the one-launch conv1 .. conv6
+MAC_PER_IMAGE["conv3_6"] = MAC_PER_IMAGE["conv34"] + MAC_PER_IMAGE["conv56"]   # conv3 .. conv6, one launch
 # algorithmic HBM bytes per image (u8 activations, fp32 input/logits)
 BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                    "conv2": 32 * 32 * 64 + 16 * 16 * 64,
@@ -70,11 +71,14 @@ BYTES_PER_IMAGE = {"conv1": 3 * 32 * 32 * 4 + 32 * 32 * 64,
                  "net": 3 * 32 * 32 * 4 + 4 * 4 * 256,
                  # one launch: fp32 input, a6 out, and the a2 / a4 hand-offs it
                  # writes and reads back through memory
-                 "conv1_6": 3 * 32 * 32 * 4 + 4 * 4 * 256 + 2 * (16 * 16 * 64 + 8 * 8 * 128)}
+                 "conv1_6": 3 * 32 * 32 * 4 + 4 * 4 * 256 + 2 * (16 * 16 * 64 + 8 * 8 * 128),
+                 # conv3 .. conv6 in one launch: a2 in, a6 out, a4 written and read back
+                 "conv3_6": 16 * 16 * 64 + 4 * 4 * 256 + 2 * 8 * 8 * 128}
 HBM_BOUND = {"conv1"}
 # launch name -> the kernel symbols it runs (rocprofv3 Kernel_Name substrings)
 KERNEL_SYMBOLS = {"conv1_6": ("convnet_convs16_kernel", "convnet_convs_kernel", "convnet_convs_sm_kernel"),
                   "conv12": ("conv12p_kernel",),
+                  "conv3_6": ("convs36_w4_kernel",),
                   # (the persistent wave-specialised kernel from two images per CU
                   # (four for conv5+6), the per-tile pair kernels below)
                   "conv34": ("convpair_ws_kernel<qcn::ConvCfg<64, 128", "convpair_kernel<qcn::ConvCfg<64, 128"),

@@ -24,60 +24,23 @@
 //  * for pooled layers a wave's four pixel tiles are the four 2x2-window
 //    quadrants of the same 32 pooled pixels, so pooling is a register max.
 #include "common.hpp"
+#include "conv_epi.hpp"
 #include <type_traits>
 #include <utility>
 #include <algorithm>
 #include <cmath>
 #include "qconvnet_abi.hpp"
 
-// weight-prefetch depth (K-steps) of the wave-specialised pair kernels; D + 1
-// must divide 18 (build-time constant, not a runtime switch)
-#ifndef QCN_PIPE34_D
-#define QCN_PIPE34_D 2
-#endif
-// diagnostic builds only (tools/build_variant.sh): 0 keeps a pair on its
-// per-tile kernel for same-process A/B against the wave-specialised one
-#ifndef QCN_WS34
-#define QCN_WS34 1
-#endif
-#ifndef QCN_WS56
-#define QCN_WS56 1
-#endif
-// 1: the separate conv5+6 launch at <= 1 image per CU on one 8-wave workgroup
-// per image (lane-pooled conv6, the form the one-launch convs use there);
-// default 0 keeps r03's cout-split form, which is faster as a launch of its
-// own (batch 256: 54.8 vs 58.8 us per forward with three launches,
-// profiles/r04_diag_small_conv56_ab.txt) — diagnostic builds only
-#ifndef QCN_SM56
-#define QCN_SM56 0
-#endif
-// weight-prefetch depth (K-steps) of the one-image conv5+6 (build-time)
-#ifndef QCN_SM56_D
-#define QCN_SM56_D 4
-#endif
-// 1: the wave-specialised pair phases on v_mfma_i32_16x16x64_i8 (r05); 0
-// keeps the 32x32x32 pipeline for same-box A/B (diagnostic builds only)
-#ifndef QCN_M16
-#define QCN_M16 1
-#endif
-// diagnostic: s_setprio of the conv B role (waves 4-7, the second-dispatched
-// half) in the 16x16 pair phases; 0 leaves both roles at priority 0
-#ifndef QCN_WS16_BPRIO
-#define QCN_WS16_BPRIO 0
-#endif
-
 namespace qcn {
 
+// weight-prefetch depth (K-steps) of the 32x32 wave-specialised pair kernels;
+// D + 1 must divide 18
+constexpr int kPipeD = 2;
+// K-step prefetch depth of the one-image conv5+6 (convnet_convs_sm_kernel)
+constexpr int kSm56D = 4;
 // conv12 producer waves' issue priority (swept: 1-3 within noise, 2 best;
 // 0 is ~20 % slower, profiles/r01_diag_conv12_prio_sweep_v16.txt)
-#ifndef QCN_PROD_PRIO
-#define QCN_PROD_PRIO 2
-#endif
-constexpr int kProdPrio = QCN_PROD_PRIO;
-// diagnostic: the conv12 consumer's priority during its epilogue (0: unchanged)
-#ifndef QCN_C2_EPI_PRIO
-#define QCN_C2_EPI_PRIO 0
-#endif
+constexpr int kProdPrio = 2;
 
 // Patch layout knobs (chosen per layer by an offline bank-conflict search so
 // that every ds_read_b128 of an MFMA operand is conflict-free):
@@ -149,27 +112,6 @@ struct ConvCfg {
     return seg * SS + prow * RS + cpos * PS;
   }
 };
-
-struct ConvEpi {
-  const float* u;      // [COUT]
-  const float* v;      // [COUT]
-  const float* mult;   // [COUT]
-  const int* corr;     // [COUT] (128 - zp_x) * sum_k w[k]
-  int zp_y, lo;        // output zero point, lower clamp (zp_y if relu else 0)
-  int qdq;             // 0: write requantized u8; 1: apply qdq_next; 2: as 1, with the
-                       // exact one-fma form below (qdq_affine, set on the host)
-  float s1; int z1; float inv2; int z2;
-  int kmajor;          // 1: write y as [f / 32][image][32] (f = NHWC flatten index)
-  // qdq == 2: requant + QDQ hand-off of an accumulator with ab = (acc + u v) m is
-  // cvt_pk(med3(fma(rint(ab), qa, qb), glo, ghi)) — zp_y, lo, the dequantize,
-  // ReLU and the next stub's quantize folded into one fma and one med3
-  float qa, qb, glo, ghi;
-};
-
-// the QDQ hand-off after the requant, in the one-fma form (qdq == 2)
-QCN_DEV float qdq_aff_f(float ab, const ConvEpi& ep) {
-  return __builtin_amdgcn_fmed3f(__builtin_fmaf(__builtin_rintf(ab), ep.qa, ep.qb), ep.glo, ep.ghi);
-}
 
 // Requantize one 32(cout) x 32(pixel) accumulator tile (optionally the max of
 // four quadrant tiles) and write it to the LDS output image [pixel][cout]:
@@ -300,9 +242,6 @@ QCN_DEV void epilogue_tile_k(const v16i* accs, const EpiK& K, const ConvEpi& ep,
   else
     *reinterpret_cast<uint4*>(orow + co_base + 16 * hi) = make_uint4(w[0], w[1], w[2], w[3]);
 }
-
-__host__ __device__ inline bool epi_fast(const ConvEpi& ep) { return ep.zp_y == 0 && ep.lo == 0 && ep.qdq == 0; }
-inline int epi_mode(const ConvEpi& ep) { return ep.qdq == 2 ? 2 : (epi_fast(ep) ? 1 : 0); }
 
 template <int NQ, bool XORIN = false, bool D32 = false, bool GWT = false>
 QCN_DEV void epilogue_tile_kf(const v16i* accs, const EpiK& K, const ConvEpi& ep, int co_base,
@@ -1078,45 +1017,6 @@ void convpair_ga_split_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp,
   convpair_ga_split_body<CA, CB, D, COUTB>((int)blockIdx.x, x, nimg, x_zp, wa, epa, xb_zp, wb, epb, y);
 }
 
-// Epilogue constants of 4 consecutive output channels from an LDS copy
-// (u | v | mult, cout floats each).
-struct EpiG {
-  float4 u, v, m;
-};
-QCN_DEV EpiG load_epig(const float* ek, int cout, int co) {
-  return {*reinterpret_cast<const float4*>(ek + co), *reinterpret_cast<const float4*>(ek + cout + co),
-          *reinterpret_cast<const float4*>(ek + 2 * cout + co)};
-}
-QCN_DEV float f4e(const float4& f, int e) { return e == 0 ? f.x : (e == 1 ? f.y : (e == 2 ? f.z : f.w)); }
-
-// Compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1 (a
-// guaranteed unroll, so every register-array index below is a constant).
-template <class F, int... I>
-QCN_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-QCN_DEV void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// One requantized output into byte e of wd (epilogue_tile_k's arithmetic,
-// EM as there).
-template <int EM>
-QCN_DEV uint32_t rq_elem(int a, const EpiG& K, int e, const ConvEpi& ep, uint32_t wd) {
-  const float u = f4e(K.u, e), v = f4e(K.v, e), m = f4e(K.m, e);
-  if constexpr (EM != 0) {
-    float f = __builtin_fmaf(u, v, (float)a);
-    f = f * m;
-    if constexpr (EM == 2) f = qdq_aff_f(f, ep);
-    return __builtin_amdgcn_cvt_pk_u8_f32(f, e, wd);
-  } else {
-    float q = requant_f(a, u, v, m, (float)ep.zp_y, (float)ep.lo);
-    if (ep.qdq) q = qdq_next_f(q, ep.s1, (float)ep.z1, ep.inv2, (float)ep.z2);
-    return __builtin_amdgcn_cvt_pk_u8_f32(q, e, wd);
-  }
-}
-
 // One conv of the pipeline over a staged patch: 2 * C::NCH K-steps of 8
 // MFMAs (64 couts x 128 pixels per wave), A fragments from registers (ga,
 // steps 0..D-1 already in flight), B fragments from the patch; fill(k) runs
@@ -1195,16 +1095,6 @@ QCN_DEV void p34_stamp(int kind, int& idx, unsigned long long t) {
 #define P34_STAMP()
 #endif
 
-// LDS writes of this wave complete, then the workgroup barrier (global stores
-// stay in flight: no vmcnt drain, unlike __syncthreads).
-QCN_DEV void lds_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // --------------------------------------------------------------------------
 // Two convolutions of a block with wave-specialised roles (persistent; the
 // headline's conv3+conv4 and conv5+conv6 at batch 1024).  One 8-wave
@@ -1259,7 +1149,7 @@ struct PairWs {
 // Workgroup b of G: its tiles are k = 0 .. T-1.  Image of segment s of tile k:
 // (b + k G) SEGS + s (ILV = false: tile b + k G of the batch), or
 // b + (k SEGS + s) G (ILV = true: the images b, b + G, b + 2G, ... that the
-// earlier phases of convnet_convs_kernel gave this workgroup, paired up).
+// earlier phases of the one-launch kernel gave this workgroup, paired up).
 template <class CA, class CB, int D, int FA, int FB, bool KMAJOR, bool ILV = false>
 QCN_DEV void convpair_ws_body(int b, int G, const uint8_t* __restrict__ x, int nimg, int x_zp,
                               const int8_t* __restrict__ wa, const ConvEpi& epa, int xb_zp,
@@ -1628,14 +1518,8 @@ QCN_DEV void pipe_job16(const uint8_t* patch, const int* corr, wt_rsrc_t wr, wt_
     return *reinterpret_cast<const v4i*>(patch + lb + X::jofs(j) + PatchAddr<C>::delta(tap, j) + cb * 64);
   };
   auto issue = [&](wt_rsrc_t r, int s, int slot) {
-#if defined(QCN_EXP_WA_SAME)   // diagnostic probe only (wrong results): every step loads step 0's chunk
-    s = 0;
-#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#if defined(QCN_EXP_WA_NONE)   // diagnostic probe only (wrong results): no weight loads after the first
-      if (s != 0) { ga[slot][i] = ga[slot ^ 1][i]; continue; }
-#endif
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, s * C::WBUF + i * 1024, 0);
       ga[slot][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
     }
@@ -1924,7 +1808,6 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
       lds_barrier();
     }
   } else {
-    if (QCN_WS16_BPRIO) __builtin_amdgcn_s_setprio(QCN_WS16_BPRIO);
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
       if constexpr (!P::DOUBLE_A) lds_barrier();
@@ -2508,7 +2391,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     conv_mainloop_res<C>(pb, lds + L::OFF_W, reinterpret_cast<const int*>(lds + L::OFF_CORR2),
                          wave, ln, acc);
     C12_STAMP(((t >> 1) - t0) / ts * 2 + (t & 1) + 1, 2);
-    if constexpr (QCN_C2_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(QCN_C2_EPI_PRIO);
     const int n = t >> 1, h = t & 1;
     const float* ek2 = reinterpret_cast<const float*>(lds + L::OFF_EPI2);
     uint8_t* dst = y + ((long)n * 256 + h * 128 + wave * 32 + l32) * 64;
@@ -2518,7 +2400,6 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     for (int i = 0; i < 2; ++i)
       epilogue_tile_kf<4, false, false, true>(acc[i], load_epik_lds(ek2, 64, i * 32, hi), ep2, i * 32, hi,
                                               dst, wbase, woff);
-    if constexpr (QCN_C2_EPI_PRIO > 0) __builtin_amdgcn_s_setprio(0);
   };
 
   if (producer && T > 0) stage_load(tile_of(0));
@@ -2607,9 +2488,7 @@ using WsA5 = ConvCfg<128, 256, 8, false, 1, 16, 224, 0, false>;
 using WsB6 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-[[maybe_unused]] constexpr int kConvnetLds = cmax(Conv12P::LDS, cmax(PairWs<WsA3, WsB4, QCN_PIPE34_D>::LDS,
-                                                   PairWs<WsA5, WsB6, QCN_PIPE34_D>::LDS));
-[[maybe_unused]] constexpr int kConvnet16Lds = cmax(Conv12P::LDS, cmax(PairWs16<W16A3, W16B4>::LDS, PairWs16<W16A5, W16B6>::LDS));
+constexpr int kConvnet16Lds = cmax(Conv12P::LDS, cmax(PairWs16<W16A3, W16B4>::LDS, PairWs16<W16A5, W16B6>::LDS));
 constexpr int kConvnetSmLds = cmax(Conv12P::LDS, cmax(PairCfg<SmA3, SmB4>::LDS, PairGaCfg<SmA5, SmB6>::LDS));
 
 // Diagnostic builds only (tools/clock: -DQCN_CONVNET_STAMP): s_memtime /
@@ -2638,29 +2517,6 @@ QCN_DEV void phase_boundary() {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_setprio(0);
   __syncthreads();
-}
-
-template <int EM, bool KMAJOR>
-__global__ __launch_bounds__(512, 1)
-void convnet_convs_kernel(const float* __restrict__ x, int nimg, float in_inv, QCN_C16_PARAMS,
-                          uint8_t* __restrict__ a2, uint8_t* __restrict__ a4, uint8_t* __restrict__ a6) {
-  // conv3+4 (ILV false) reads only its own workgroup's a2 because its tiles
-  // are single images: tile b + kG is image b + kG, as conv12p wrote it
-  static_assert(PairWs<WsA3, WsB4, QCN_PIPE34_D>::SEGS == 1, "conv3+4 tile k of workgroup b is image b + kG");
-  const int b = (int)blockIdx.x, G = (int)gridDim.x;
-  const int T = b < nimg ? 2 * ((nimg - 1 - b) / G + 1) : 0;
-  C16_STAMP(0);
-  conv12p_body(b, G, T, x, nimg, in_inv, z0, w0, e0, z1, w1, e1, a2);
-  phase_boundary();
-  C16_STAMP(1);
-  convpair_ws_body<WsA3, WsB4, QCN_PIPE34_D, EM, EM, false>(b, G, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
-  phase_boundary();
-  C16_STAMP(2);
-  convpair_ws_body<WsA5, WsB6, QCN_PIPE34_D, EM, EM, KMAJOR, true>(b, G, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
-#ifdef QCN_CONVNET_STAMP
-  __syncthreads();
-#endif
-  C16_STAMP(3);
 }
 
 // The same launch with the pair phases on the 16x16x64 pipeline (r05).  The
@@ -2703,7 +2559,7 @@ void convnet_convs_sm_kernel(const float* __restrict__ x, int nimg, float in_inv
   convpair_body<SmA3, SmB4>(b, a2, nimg, z2, w2, e2, z3, w3, e3, a4);
   phase_boundary();
   C16_STAMP(2);
-  convpair_ga_body<SmA5, SmB6, QCN_SM56_D>(b, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
+  convpair_ga_body<SmA5, SmB6, kSm56D>(b, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif
@@ -3105,13 +2961,9 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     using A3 = WsA3;
     using B4 = WsB4;
     // two or more images per CU: the persistent wave-specialised kernel
-    if (QCN_WS34 && nimg >= 2 * ncu) {
-      if (QCN_M16)
-        return launch_pair_ws<A3, B4, QCN_PIPE34_D, W16A3, W16B4>(x, nimg, x_zp, wa_packed, epa, xb_zp,
-                                                                  wb_packed, epb, kmajor != 0, y, st, ncu);
-      return launch_pair_ws<A3, B4, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
-                                                  kmajor != 0, y, st, ncu);
-    }
+    if (nimg >= 2 * ncu)
+      return launch_pair_ws<A3, B4, kPipeD, W16A3, W16B4>(x, nimg, x_zp, wa_packed, epa, xb_zp,
+                                                          wb_packed, epb, kmajor != 0, y, st, ncu);
     return launch_pair<A3, B4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
@@ -3119,13 +2971,6 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     // into registers 4 K-steps ahead (convpair_ga_kernel)
     using A1 = WsA5;
     using B1 = WsB6;
-    // at or below one image per CU (QCN_SM56): one image per 8-wave workgroup
-    // (conv5 and conv6 as 32-cout x 64-pixel wave tiles, conv6 lane-pooled) —
-    // no recomputation, but every workgroup streams all 885 KB of conv5+6
-    // weights from L2 for one image
-    if (QCN_SM56 && nimg <= ncu)
-      return launch_pair_ga<SmA5, SmB6, QCN_SM56_D>(
-          x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // default: conv6's couts split over two 4-wave workgroups per image pair,
     // each computing all of conv5 (4/3 of the MFMAs, half the weight bytes per
     // image)
@@ -3133,13 +2978,9 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
       return launch_pair_ga_split<A1, ConvCfg<256, 128, 8, true, 1, 16, 32, 64, true, 1>, 4, 256>(
           x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // two or more image pairs per CU: the persistent wave-specialised kernel
-    if (QCN_WS56 && nimg >= 4 * ncu) {
-      if (QCN_M16)
-        return launch_pair_ws<A1, B1, QCN_PIPE34_D, W16A5, W16B6>(x, nimg, x_zp, wa_packed, epa, xb_zp,
-                                                                  wb_packed, epb, kmajor != 0, y, st, ncu);
-      return launch_pair_ws<A1, B1, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
-                                                  kmajor != 0, y, st, ncu);
-    }
+    if (nimg >= 4 * ncu)
+      return launch_pair_ws<A1, B1, kPipeD, W16A5, W16B6>(x, nimg, x_zp, wa_packed, epa, xb_zp,
+                                                          wb_packed, epb, kmajor != 0, y, st, ncu);
     return launch_pair_ga<A1, B1, 4>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
   return QCN_ERR_UNSUPPORTED;
@@ -3288,13 +3129,8 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
     return hipGetLastError() == hipSuccess ? QCN_OK : QCN_ERR_HIP;
   }
   static bool attr_done[4][QCN_MAX_DEV] = {};
-#if QCN_M16
 #define QCN_C16_KERNEL qcn::convnet_convs16_kernel
 #define QCN_C16_LDS qcn::kConvnet16Lds
-#else
-#define QCN_C16_KERNEL qcn::convnet_convs_kernel
-#define QCN_C16_LDS qcn::kConvnetLds
-#endif
 #define QCN_C16(EM_, KM_)                                                                          \
   if (em == EM_ && (kmajor != 0) == KM_) {                                                         \
     auto k = QCN_C16_KERNEL<EM_, KM_>;                                                             \

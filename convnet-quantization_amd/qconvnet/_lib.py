@@ -58,6 +58,7 @@ SIGNATURES = {
                                     i32, C.POINTER(QDQ), vp, vp]),
     "qcn_convnet_convs_f32_nchw": (i32, [vp, i32, f32, i32, C.POINTER(ConvLayer), vp, vp, vp, i32, vp]),
     "qcn_convnet_convs_form": (i32, [i32, f32, i32, C.POINTER(ConvLayer), i32]),
+    "qcn_convs36_u8s8": (i32, [vp, i32, C.POINTER(ConvLayer), vp, vp, i32, vp]),
     "qcn_conv1_f32_nchw": (i32, [vp, i32, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,
                                  C.POINTER(QDQ), vp, vp, vp]),
     "qcn_conv12_fused_f32_nchw": (i32, [vp, i32, f32, i32, vp, vp, vp, vp, vp, i32, i32,

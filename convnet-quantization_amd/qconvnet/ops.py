@@ -211,6 +211,29 @@ def convnet_convs(x, in_scale, in_zp, layers, a2, a4, a6, kmajor=True):
     return True
 
 
+def convs36(a2, layers, a4, a6, kmajor=True):
+    """conv3 .. conv6 in one persistent launch of one-wave-per-SIMD
+    workgroups (qcn_convs36_u8s8): a2 [n,16,16,64] u8 NHWC in, a4 written,
+    conv6's pooled output into a6 (chunk-major [128, n, 32] when kmajor, else
+    NHWC [n, 4, 4, 256]).  ``layers``: conv_layers() (its conv3 .. conv6
+    entries are used).  Returns False when the launch does not apply (mixed
+    epilogue forms)."""
+    _need(a2, torch.uint8, "convs36.a2")
+    n = a2.shape[0]
+    if tuple(a2.shape[1:]) != (16, 16, 64):
+        raise ValueError("convs36 expects a2 [n,16,16,64]")
+    _need(a4, torch.uint8, "convs36.a4")
+    _need(a6, torch.uint8, "convs36.a6")
+    if a4.numel() != n * 8 * 8 * 128 or a6.numel() != n * 4096:
+        raise ValueError("convs36: a4 / a6 sizes do not match the batch")
+    l3 = C.cast(C.byref(layers, 2 * C.sizeof(_lib.ConvLayer)), C.POINTER(_lib.ConvLayer))
+    rc = lib().qcn_convs36_u8s8(_ptr(a2), n, l3, _ptr(a4), _ptr(a6), int(bool(kmajor)), _stream())
+    if rc == _lib.QCN_ERR_UNSUPPORTED:
+        return False
+    check(rc, "convs36")
+    return True
+
+
 def convnet_convs_form(n, in_scale, in_zp, layers, kmajor=True):
     """Host query (no launch, current device): 1 when convnet_convs() runs one
     image per workgroup for batch n, 2 the persistent form, 0 when it would

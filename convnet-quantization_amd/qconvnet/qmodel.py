@@ -221,6 +221,11 @@ class QuantizedConvNet:
         # QuantStub + conv1 .. conv6 as one persistent launch where the library
         # takes it (>= 4 images per CU; False: conv12 + the two pair launches)
         self.fuse_convs = True
+        # conv12 as its own launch, then conv3 .. conv6 in one launch of
+        # one-wave-per-SIMD workgroups (qcn_convs36_u8s8, r06) instead of the
+        # one-launch conv1 .. conv6 (fuse_convs), from 4 images per CU
+        self.convs_w4 = False
+        self._w4_ok = {}         # batch size -> whether the conv3 .. conv6 launch ran
         self._convs_ok = {}      # batch size -> whether the one-launch convs ran
         self._conv_layers = None
         self._bufs = {}
@@ -308,6 +313,8 @@ class QuantizedConvNet:
         """Names of the launches run() marks, in order (conv1+conv2 are one
         launch when fused, conv3+conv4 / conv5+conv6 one launch each when
         paired, fc1+fc2 one "fc12" slot for the fused head)."""
+        if self._w4(x_shape, keep):
+            return ("conv12", "conv3_6", "fc12") if self._head(x_shape[0], keep) else ("conv12", "conv3_6", "fc1", "fc2")
         if self._convs(x_shape, keep) and self._convs_form(x_shape[0], keep):
             return ("conv1_6", "fc12") if self._head(x_shape[0], keep) else ("conv1_6", "fc1", "fc2")
         names = list(self.KERNELS_FUSED if self._fused(x_shape) else self.KERNELS)
@@ -356,6 +363,16 @@ class QuantizedConvNet:
                                             kmajor=self._head(n, keep)) > 0
         return ok
 
+    def _w4(self, x_shape, keep):
+        """conv12 + the one-wave-per-SIMD conv3 .. conv6 launch applies: from 4
+        images per CU (below that its 4-image conv5+6 tiles are mostly empty),
+        unless the library declined this batch size before."""
+        n = x_shape[0]
+        if not (self.convs_w4 and self._fused(x_shape) and self._pairs(keep) and self._w4_ok.get(n, True)):
+            return False
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return n >= 4 * ncu
+
     def _convs(self, x_shape, keep):
         """The one-launch conv1 .. conv6 applies to this forward (the library
         may still decline the batch size: _convs_ok records that per size)."""
@@ -388,8 +405,23 @@ class QuantizedConvNet:
         d = L[0]
         names = ["a2", "a3", "a4", "a5", "a6"]
         head = self._head(n, keep)
-        convs_done = False
-        if self._convs(x.shape, keep) and self._convs_ok.get(n, True):
+        convs_done = conv12_done = False
+        if self._w4(x.shape, keep):
+            if self._conv_layers is None:
+                self._conv_layers = ops.conv_layers(L, self.in_zp)
+            ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])
+            mark()
+            if head and "a6k" not in b:
+                b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
+            out6 = b["a6k"] if head else b["a6"]
+            w4_done = ops.convs36(b["a2"], self._conv_layers, b["a4"], out6, kmajor=head)
+            self._w4_ok[n] = w4_done
+            if w4_done:
+                mark()
+                prev, first, convs_done = b["a6"], 6, True
+            else:   # (mixed epilogue forms) the pair launches from a2
+                prev, first, conv12_done = b["a2"], 2, True
+        elif self._convs(x.shape, keep) and self._convs_ok.get(n, True):
             if head and "a6k" not in b:
                 b["a6k"] = torch.empty((128, n, 32), dtype=torch.uint8, device=self.device)
             if self._conv_layers is None:
@@ -400,7 +432,7 @@ class QuantizedConvNet:
             if convs_done:
                 mark()
                 prev, first = b["a6"], 6
-        if convs_done:
+        if convs_done or conv12_done:
             pass
         elif self._fused(x.shape):
             ops.conv12_fused(x, self.in_scale, self.in_zp, L[0], L[1], out=b["a2"])

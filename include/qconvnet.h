@@ -137,6 +137,18 @@ int qcn_convnet_convs_f32_nchw(const float* x, int nimg, float in_scale, int in_
                                const qcn_conv_layer_t* layers, uint8_t* a2, uint8_t* a4, uint8_t* a6,
                                int kmajor, void* stream);
 
+/* A5+A6+A10 x4 — conv3 .. conv6 of SimpleConvNet (baseline_model.py:20-33,
+ * :64-75) in one persistent launch of 256-thread workgroups (one wave per
+ * SIMD, 64-cout x 256-pixel wave tiles, r06): a2 u8 NHWC [nimg,16,16,64] in
+ * (qcn_conv12_fused_f32_nchw's output), a4 ([nimg,8,8,128]) written on the
+ * way, conv6's pooled output into a6 as qcn_convnet_convs_f32_nchw writes it
+ * (chunk-major when kmajor).  layers: the four layers conv3 .. conv6
+ * (layers[0].x_zp = conv2's output zero point).  Bit-exact with the pair
+ * launches.  QCN_ERR_UNSUPPORTED unless conv3..conv6 are all on the FBGEMM
+ * fast epilogue or all on the one-fma QDQ form. */
+int qcn_convs36_u8s8(const uint8_t* a2, int nimg, const qcn_conv_layer_t* layers, uint8_t* a4, uint8_t* a6,
+                     int kmajor, void* stream);
+
 /* Host query (no launch): which form qcn_convnet_convs_f32_nchw takes for
  * these arguments on the current device — 1 one image per workgroup, 2 the
  * persistent form, or the error it would return (QCN_ERR_UNSUPPORTED,

@@ -159,7 +159,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
           1, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
     // the product's wave-specialised kernel, built here with its stamps
     return launch_pair_ws<ConvCfg<64, 128, 16, false, 2, 16, 96, 0, false>,
-                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>, QCN_PIPE34_D>(
+                          ConvCfg<128, 128, 16, true, 2, 16, 32, 0, true>, kPipeD>(
         x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, kmajor != 0, y, st, ncu);
   }
   if (hw == 8 && cin == 128 && cmid == 256 && cout == 256) {
@@ -178,7 +178,7 @@ int qcn_conv3x3_pair_u8s8(const uint8_t* x, int nimg, int hw, int cin, int x_zp,
     using B1 = ConvCfg<256, 256, 8, true, 1, 16, 32, 64, true>;
     g_last56_ws = nimg >= 4 * ncu;
     if (g_last56_ws)
-      return launch_pair_ws<A1, B1, QCN_PIPE34_D>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
+      return launch_pair_ws<A1, B1, kPipeD>(x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb,
                                                   kmajor != 0, y, st, ncu);
     return launch_pair_ga_stamped<A1, B1, 4>(2, x, nimg, x_zp, wa_packed, epa, xb_zp, wb_packed, epb, y, st);
   }
