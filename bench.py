@@ -629,9 +629,62 @@ class StepLoop:
                         "the next batch's forward"}
 
 
+def launch_ranks(argv, n):
+    """``--gpus N`` (N > 1) without torchrun's env: start N ranks through
+    torch.distributed.run as a CHILD process, from a parent that has not
+    touched the GPU (no exec), and return its exit code.  Rank 0 of the child
+    prints the one JSON line.  Never run one rank and label it N."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def main_rehearse(args):
+    """--rehearse: the multi-rank harness on CPU over gloo (launcher, barrier,
+    StepLoop with the asynchronous logits all-gather, max-over-ranks timing,
+    the N > 1 fields of the line).  Each rank's "forward" is a fixed fp32
+    matmul of its shard standing in for the model: the line it prints is a
+    rehearsal of the plumbing, not a measurement of the int8 path."""
+    from qconvnet import dist as qd
+    rank, world, _ = qd.init("gloo")
+    B = args.batch
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.rand((B, 3 * 32 * 32), generator=g)
+    w = torch.rand((3 * 32 * 32, 10), generator=torch.Generator().manual_seed(0))
+
+    def forward(marks=None, slot=0):
+        return x @ w
+
+    loop = StepLoop(forward, world, "cpu")
+    warm_run = ramp_warmup(loop.step, loop.drain, args.warmup, world, "cpu", 0.0, sync=loop.sync)
+    elapsed, rank_ms = loop.timed(args.steps)
+    result = {"metric": "harness rehearsal (CPU, gloo): not the int8 path", "value": world * B * args.steps / elapsed,
+              "unit": "rows/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "warmup_steps_run": warm_run, "ms_per_step": elapsed / args.steps * 1e3,
+              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+              "data": "rehearsal", "config": {"workload": "rehearsal", "global_batch": world * B,
+                                              "per_gpu_batch": B, "parallelism": f"dp{world}"}}
+    if world > 1:
+        result["rank_ms_per_step"] = rank_ms
+        result["allgather"] = loop.allgather_timing(forward(), 3)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU; without torchrun's WORLD_SIZE, N > 1 starts "
+                         "torch.distributed.run with N ranks as a child process")
+    ap.add_argument("--rehearse", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps K (default 400 for the SimpleConvNet workloads, 50 for "
                          "ResNet-50: each timed region pays ~0.15-0.2 ms of start-up after its "
@@ -675,6 +728,10 @@ def main():
         args.batch = {"convnet": 1024, "qdq": 256, "resnet50": 512}[args.workload]
     if args.steps is None:
         args.steps = 50 if args.workload == "resnet50" else 400
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if args.rehearse:
+        return main_rehearse(args)
     if args.workload == "resnet50":
         return main_resnet(args)
 
@@ -682,10 +739,10 @@ def main():
     from qconvnet import dist as qd
 
     rank, world, local = qd.init()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: the line would mislabel the run")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world != args.gpus and rank == 0:
-        print(f"# note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}", file=sys.stderr)
 
     mode = "qdq" if args.workload == "qdq" else "static"
     model, sd = build_model(rank, dev, args.per_channel, args.spec_file, mode)

@@ -96,3 +96,29 @@ def test_bench_step_loop_two_ranks_matches_single_process():
         assert d["slots"][:-1] == [k % 2 for k in range(len(d["slots"]) - 1)]
     # every rank took the same number of steps (their all-gathers paired up)
     assert len(res[0]["slots"]) == len(res[1]["slots"])
+
+
+def test_bench_gpus_2_without_torchrun_starts_two_ranks():
+    """`python bench.py --gpus 2` with no torchrun env starts torch.distributed.run
+    with two ranks as a child (never one rank labelled two): the line reports
+    n_gpus 2 and both ranks' step times.  The rehearsal mode runs the harness
+    on CPU over gloo with a stand-in forward."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse",
+                        "--steps", "3", "--warmup", "1", "--batch", "4"], cwd=root, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout          # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert len(d["rank_ms_per_step"]) == 2 and all(v > 0 for v in d["rank_ms_per_step"])
+    assert d["config"]["global_batch"] == 8
+    assert d["allgather"]["bytes_per_rank"] == 4 * 10 * 4
