@@ -484,6 +484,8 @@ def pmc_counters(model, sd, args, names, timeout=150):
                     res[n]["clock_probe_ms"] = c["ms"]
                 if "phase_table" in c:
                     res[n]["phase_table"] = c["phase_table"]
+                if "layer_table" in c:
+                    res[n]["layer_table"] = c["layer_table"]
         except Exception as e:
             errors.append(f"clock: {e}")
     finally:
@@ -905,6 +907,17 @@ def main():
                      "from the stamped diagnostic copy (tools/clock_probe.py), its MFMA cycles per SIMD, "
                      "MFMA issue at the clock the chip holds in it, and frac = issue x clock / 2.4 GHz"),
             **{k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in ph.items()}}
+        lt = kern.get("conv1_6", {}).get("layer_table")
+        if lt:
+            result["phases"]["layers"] = {
+                "note": ("conv1 .. conv6 each against its own bound (SURVEY §8(d)): inside the one launch the two "
+                         "convs of a phase run on different waves of the same SIMDs at once, so a layer's row is "
+                         "its role's busy cycles (stamped diagnostic copy, median over workgroups), its MFMA cycles "
+                         "per SIMD, the MFMA issue while busy and frac = issue x the phase's held clock / 2.4 GHz; "
+                         "conv1 is HBM-bound and its frac is its algorithmic bytes per busy time over 8 TB/s "
+                         "(tools/clock_probe.py layer_table)"),
+                **{k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                   for k, v in lt.items()}}
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baselines(sd, model, args.cpu_seconds)
         result["cpu_baseline"] = cb["static_ptq"]
@@ -934,7 +947,9 @@ def extra_configs(args):
     out = {}
     for key, wl in (("configs[1]", "qdq"), ("configs[4]", "resnet50")):
         cmd = [sys.executable, os.path.abspath(__file__), "--workload", wl, "--no-cpu"]
-        if args.no_pmc:
+        # the ResNet child's own two rocprofv3 counter passes would not fit its
+        # time limit beside its run: its line keeps HIP-event times only
+        if args.no_pmc or wl == "resnet50":
             cmd.append("--no-pmc")
         t0 = time.perf_counter()
         try:
@@ -945,7 +960,10 @@ def extra_configs(args):
                 out[key] = {"error": f"exit {p.returncode}: {p.stderr[-300:]}"}
                 continue
             d = json.loads(line)
-        except Exception as e:   # the metric above stands without these fields
+        except subprocess.TimeoutExpired:   # the metric above stands without these fields
+            out[key] = {"error": f"timeout: the child ran past --extra-timeout {args.extra_timeout:.0f} s"}
+            continue
+        except Exception as e:
             out[key] = {"error": f"{type(e).__name__}: {e}"}
             continue
         keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "sustained", "config",
@@ -1118,8 +1136,9 @@ def main_resnet(args):
             "algorithmic_bytes": conv_bytes * B,
             "note": "int8 TOPS in the TFLOP/s slot; achieved = 2*sum(conv MAC)*batch / summed "
                     "HIP-event conv time; stem MACs counted at the packed K=224 actually issued; "
-                    "algorithmic_bytes counts every conv's input and output layer by layer (the fused "
-                    "reduces do not re-read their input)"}
+                    "algorithmic_bytes counts every conv's input and output layer by layer, including "
+                    "the three fused reduces' 256-channel inputs, which in the fused launches never "
+                    "leave the chip"}
     if rank == 0 and world == 1 and not args.no_pmc:
         if under_profiler():
             roof["pmc_error"] = "skipped: this run is itself under rocprofv3"

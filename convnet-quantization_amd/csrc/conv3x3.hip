@@ -1451,6 +1451,29 @@ void convpair_ws_kernel(const uint8_t* __restrict__ x, int nimg, int x_zp, const
 // reads (tools/lds_banks.py: every ds_read_b128 conflict-free needs a pixel
 // stride of 16 B x 2 mod 4, i.e. Cin + 32).
 
+// Diagnostic builds only (tools/clock: -DQCN_CONVNET_STAMP): s_memtime of lane
+// 0 of wave 0 (conv A role) and wave 4 (conv B role) in every period of the
+// 16x16 pair phases: [wg][phase: conv3+4, conv5+6][role][period][k], k = 0 the
+// period's start (after its barrier), 1 the role's first piece done (A: the
+// conv job; B: the previous tile's pooled epilogue), 2 its second (A: the
+// epilogue and input hand-off; B: the conv job).  Plain vector stores into a
+// buffer nothing else reads; the product library compiles none of it.
+#ifdef QCN_CONVNET_STAMP
+__device__ unsigned long long g_ws16_stamp[4096][2][2][8][3];
+QCN_DEV void ws16_stamp(int ph, int p, int k) {
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int w = threadIdx.x >> 6;
+  if ((w == 0 || w == 4) && lane == 0 && blockIdx.x < 4096 && p < 8) {
+    volatile unsigned long long* d = &g_ws16_stamp[blockIdx.x][ph][w >> 2][p][k];
+    *d = t + lane;
+  }
+}
+#define WS16_STAMP(p, k) ws16_stamp(CA::kCin == 64 ? 0 : 1, (p), (k))
+#else
+#define WS16_STAMP(p, k)
+#endif
+
 // Patch slot of (wave wp, block j, lane pixel p) of conv C (output pixel
 // coordinates, the 3x3 taps add PatchAddr<C>::delta).  Every layout used is
 // affine: slot(wp, j, p) = slot(wp, 0, p) + jofs(j), checked at compile time,
@@ -1623,10 +1646,13 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
     const int pix = (p / CH16) % IMG;
     return CA::slot(p / (IMG * CH16), pix / W + 1, pix % W + 1) + (p % CH16) * 16;
   };
-  uint4 sv[4];
+  // tile 0's input (A waves), loaded first so the latency hides under the
+  // set-up; this copy dies at the first write: the A-role loop keeps its own
+  // (a value live across the other role's branch would be spilled around it)
+  uint4 sv0[4];
   if (role == 0 && T > 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(0, q));
+    for (int q = 0; q < 4; ++q) sv0[q] = *reinterpret_cast<const uint4*>(in_src(0, q));
   }
   float* eka = reinterpret_cast<float*>(lds + P::OFF_EA);
   float* ekb = reinterpret_cast<float*>(lds + P::OFF_EB);
@@ -1656,11 +1682,6 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
     return dst ? reinterpret_cast<float4*>(crb) + e
                : const_cast<float4*>(reinterpret_cast<const float4*>(epb.corr) + e);
   };
-  if (role == 1) {
-#pragma unroll
-    for (int k = 0; k < TPT; ++k)
-      if (rt + 256 * k < NTAB) tval[k] = *tab(rt + 256 * k, false);
-  }
   {  // zero-point halos of every buffer of both patches (never overwritten)
     const uint32_t pa4 = xor80(splat_u8(x_zp)), pb4 = xor80(splat_u8(xb_zp));
     auto halo = [&](auto cfg, uint8_t* base, int nbuf, int pbytes, uint32_t pad) {
@@ -1679,7 +1700,13 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
     halo(CA{}, lds + P::OFF_PA, P::DOUBLE_A ? 2 : 1, P::PA, pa4);
     halo(CB{}, lds + P::OFF_PB, 2, P::PB, pb4);
   }
+  // the epilogue tables (u | v | mult of both convs, both corr) in 16-B
+  // pieces over the B-role threads, after the halos (values held across the
+  // halo loop were spilled)
   if (role == 1) {
+#pragma unroll
+    for (int k = 0; k < TPT; ++k)
+      if (rt + 256 * k < NTAB) tval[k] = *tab(rt + 256 * k, false);
 #pragma unroll
     for (int k = 0; k < TPT; ++k)
       if (rt + 256 * k < NTAB) *tab(rt + 256 * k, true) = tval[k];
@@ -1691,24 +1718,24 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
   const int voff = (wc * 64 + p16) * 64 + g * 16;
   auto pa_buf = [&](int j) { return lds + P::OFF_PA + (P::DOUBLE_A ? (j & 1) * P::PA : 0); };
   auto pb_buf = [&](int j) { return lds + P::OFF_PB + (j & 1) * P::PB; };
-  auto write_in = [&](uint8_t* pa) {
+  auto write_in = [&](uint8_t* pa, const uint4 (&sv)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       *reinterpret_cast<uint4*>(pa + in_dst(q)) =
           make_uint4(xor80(sv[q].x), xor80(sv[q].y), xor80(sv[q].z), xor80(sv[q].w));
   };
-
-  v4i acc[4][8];
-  v4i ga[2][4];
-  {
-    const wt_rsrc_t w0 = role == 0 ? wra : wrb;
+  // each role's first weight chunk, issued inside its own branch (the B
+  // waves' first job starts a period later, the A waves' at once)
+  auto first_chunk = [&](wt_rsrc_t w0, v4i (&ga)[2][4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(w0, voff, i * 1024, 0);
       ga[0][i] = (v4i){(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
     }
-  }
-  if (role == 0) write_in(pa_buf(0));
+  };
+
+  v4i acc[4][8];
+  if (role == 0) write_in(pa_buf(0), sv0);
   lds_barrier();
 
   // lane-derived addressing from a laundered lane id (not hoisted out of the
@@ -1790,36 +1817,50 @@ QCN_DEV void convpair_ws16_body(int b, int G, const uint8_t* __restrict__ x, int
   };
 
   if (role == 0) {
+    v4i ga[2][4];
+    first_chunk(wra, ga);
+    uint4 sv[4] = {};   // tile p + 1's input, loaded during period p
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
       if constexpr (!P::DOUBLE_A) {   // tile p's input, held since period p - 1
-        if (p >= 1 && p < T) write_in(pa_buf(p));
+        if (p >= 1 && p < T) write_in(pa_buf(p), sv);
         lds_barrier();
       }
+      WS16_STAMP(p, 0);
       if (p < T) {
         const Lane L = lanes();
         pipe_job16<CA>(pa_buf(p), L.ca, wra, wra, voff, wc, L.la, L.g, acc, ga);
+        WS16_STAMP(p, 1);
         const int kn = p + 1 < T ? p + 1 : p;
 #pragma unroll
         for (int q = 0; q < 4; ++q) sv[q] = *reinterpret_cast<const uint4*>(in_src(kn, q));
         epi_a(L, pb_buf(p));
-        if constexpr (P::DOUBLE_A) write_in(pa_buf(p + 1));
+        if constexpr (P::DOUBLE_A) write_in(pa_buf(p + 1), sv);
+        WS16_STAMP(p, 2);
       }
       lds_barrier();
     }
   } else {
+    v4i ga[2][4];
+    first_chunk(wrb, ga);
 #pragma unroll 1
     for (int p = 0; p <= T; ++p) {
       if constexpr (!P::DOUBLE_A) lds_barrier();
+      WS16_STAMP(p, 0);
       if (p >= 1) {
         const Lane L = lanes();
         if (p >= 2) epi_b(L, p - 2);
+        WS16_STAMP(p, 1);
         pipe_job16<CB>(pb_buf(p - 1), L.cb, wrb, wrb, voff, wc, L.lb, L.g, acc, ga);
+        WS16_STAMP(p, 2);
       }
       lds_barrier();
     }
     const Lane L = lanes();
     epi_b(L, T - 1);
+#ifdef QCN_CONVNET_STAMP
+    if (T + 1 < 8) { WS16_STAMP(T + 1, 0); }   // the last pooled epilogue ends here
+#endif
   }
 }
 

@@ -166,7 +166,8 @@ static_assert(W4Pair<W4A3, W4B4>::LDS == kW4Lds && W4Pair<W4A5, W4B6>::LDS == kW
 // vector stores into a buffer nothing else reads.  The product library
 // compiles none of it.
 #ifdef QCN_W4_STAMP
-__device__ unsigned long long g_w4_stamp[4096][2][32];
+__device__ unsigned long long g_w4_stamp[4096][2][32];   // s_memtime
+__device__ unsigned long long g_w4_rt[4096][2][2];       // s_memrealtime at phase start / end
 QCN_DEV void w4_stamp(int ph, int idx) {
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -175,9 +176,19 @@ QCN_DEV void w4_stamp(int ph, int idx) {
     *d = t + lane;
   }
 }
+QCN_DEV void w4_rt(int ph, int idx) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if ((threadIdx.x >> 6) == 0 && lane == 0 && blockIdx.x < 4096) {
+    volatile unsigned long long* d = &g_w4_rt[blockIdx.x][ph][idx];
+    *d = t + lane;
+  }
+}
+#define W4_RT(i) w4_rt(PH, (i))
 #define W4_STAMP(i) w4_stamp(PH, (i))
 #else
 #define W4_STAMP(i)
+#define W4_RT(i)
 #endif
 
 // The MFMA as inline asm with the accumulator TIED in place ("+a"): with the
@@ -327,6 +338,7 @@ QCN_DEV void w4_pair_body(int b, int G, const uint8_t* __restrict__ x, int nimg,
     const int pix = (p / CH16) % IMG;
     return CA::slot(p / (IMG * CH16), pix / W + 1, pix % W + 1) + (p % CH16) * 16;
   };
+  W4_RT(0);
   W4_STAMP(0);
   uint4 sv[8];   // a tile's input: eight 16-B pieces per thread
   if (T > 0) {
@@ -508,6 +520,7 @@ QCN_DEV void w4_pair_body(int b, int G, const uint8_t* __restrict__ x, int nimg,
     lds_barrier();   // every wave's conv B reads of patch B done
     W4_STAMP(5 + 5 * k);
   }
+  W4_RT(1);
 }
 
 // The launch: phase 1 (conv3 + conv4, a2 -> a4), the phase boundary (every
@@ -527,6 +540,16 @@ void convs36_w4_kernel(const uint8_t* __restrict__ a2, int nimg, const int8_t* _
 }
 
 }  // namespace qcn
+
+#ifdef QCN_W4_STAMP
+// diagnostic builds only: the stamps of the last launch, [wg][phase][32] and [wg][phase][2]
+extern "C" int qcn_w4_stamps(void* mt, void* rt, int nwg) {
+  if (!mt || !rt || nwg <= 0 || nwg > 4096) return QCN_ERR_ARG;
+  if (hipMemcpyFromSymbol(mt, HIP_SYMBOL(qcn::g_w4_stamp), (size_t)nwg * 2 * 32 * 8) != hipSuccess) return QCN_ERR_HIP;
+  if (hipMemcpyFromSymbol(rt, HIP_SYMBOL(qcn::g_w4_rt), (size_t)nwg * 2 * 2 * 8) != hipSuccess) return QCN_ERR_HIP;
+  return QCN_OK;
+}
+#endif
 
 #ifndef QCN_NO_ABI
 extern "C" int qcn_convs36_u8s8(const uint8_t* a2, int nimg, const qcn_conv_layer_t* layers, uint8_t* a4,

@@ -473,14 +473,22 @@ def conv_join_reduce(x, x_zp, layer, resid, nxt, out=None, out2=None):
     _need(x, torch.uint8, "conv_join_reduce.x")
     n, h, w, cin = x.shape
     d, e = layer, nxt
+    if d.relu:   # the unfused path (conv with resid) rejects relu with a join too
+        raise ValueError("conv_join_reduce: the joined conv takes no ReLU of its own")
     r, s_r, z_r, s_o, z_o = resid
     _need(r, torch.uint8, "conv_join_reduce.resid")
     if out is None:
         out = torch.empty((n, h, w, d.cout), dtype=torch.uint8, device=x.device)
+    _need(out, torch.uint8, "conv_join_reduce.out")
+    if tuple(out.shape) != (n, h, w, d.cout):
+        raise ValueError("conv_join_reduce: out must be [n, h, w, cout]")
     if tuple(r.shape) != tuple(out.shape):
         raise ValueError("residual operand shape differs from the conv output")
     if out2 is None:
         out2 = torch.empty((n, h, w, e.cout), dtype=torch.uint8, device=x.device)
+    _need(out2, torch.uint8, "conv_join_reduce.out2")
+    if tuple(out2.shape) != (n, h, w, e.cout):
+        raise ValueError("conv_join_reduce: out2 must be [n, h, w, next cout]")
     rc = lib().qcn_conv1x1_join_reduce_u8s8_nhwc(
         _ptr(x), n, h, w, cin, int(x_zp), _ptr(d.w), d.cout, _ptr(d.u), _ptr(d.v), _ptr(d.mult),
         _ptr(d.corr), int(d.z_y), _ptr(r), float(d.s_y), float(s_r), int(z_r), float(s_o), int(z_o),

@@ -246,7 +246,7 @@ class QuantizedResNet:
         the first reduce of layer 2)."""
         one = lambda d: (d.kh, d.kw, d.sy, d.sx, d.py, d.px) == (1, 1, 1, 1, 0, 0)
         return (one(c3) and one(c1n) and c3.cin == 64 and c3.cout == 256 and c1n.cin == 256
-                and c1n.cout in (64, 128))
+                and c1n.cout in (64, 128) and not c3.relu)
 
     def conv_layers(self):
         """Every conv launch in forward order (for MAC accounting)."""

@@ -215,6 +215,14 @@ int qcn_clock_read_c16(unsigned long long* host, int n) {
                  hipSuccess ? QCN_OK : QCN_ERR_HIP;
 }
 
+// the 16x16 pair phases' per-period role stamps of the last launch
+// ([wg][phase][role][period 0..7][k 0..2], s_memtime; see g_ws16_stamp)
+int qcn_clock_read_ws16(unsigned long long* host, int n) {
+  if (n <= 0 || n > 4096 || !host) return QCN_ERR_ARG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(qcn::g_ws16_stamp), (size_t)n * 2 * 2 * 8 * 3 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? QCN_OK : QCN_ERR_HIP;
+}
+
 // conv12p's per-iteration stamps of the last launch: [wg][consumer w0, producer
 // w4, producer w5][iteration 0..11][top, before barrier, after conv2's main loop] (s_memtime).
 int qcn_clock_read_c12(unsigned long long* host, int n) {

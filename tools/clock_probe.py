@@ -51,6 +51,63 @@ def grid_of(name, n, ncu):
     return (n + 1) // 2                # two 8x8 images per 4-wave workgroup (convpair_ga_kernel)
 
 
+def layer_table(lib, g, img_per_wg, s12, T12, phases, B):
+    """conv1 .. conv6 each against its own bound, from the
+    stamped copy's role stamps.  Inside the one launch the two convs of a
+    phase run on different waves of the same SIMDs at the same time, so each
+    layer's row is its role's BUSY time (median over workgroups, summed over
+    its tiles): conv1 the conv12 producer waves (4, 5), conv2 the consumer
+    (wave 0: main loop + pooled epilogue), conv3 / conv5 the A-role wave 0
+    (job + requant into B's patch + the next input's hand-off), conv4 / conv6
+    the B-role wave 4 (pooled epilogue + job).  mfma_issue_while_busy = the
+    layer's MFMA cycles per SIMD over those busy cycles, frac_at_2p4 = that x
+    the phase's held clock / 2.4 GHz: the int8 rate the layer runs at while it
+    runs (co-running with its phase partner).  conv1 is HBM-bound (SURVEY
+    §8(d)): its row also carries its algorithmic bytes per busy time against
+    8 TB/s."""
+    import bench
+    out = {}
+    mfma = lambda n: bench.MAC_PER_IMAGE[n] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)   # noqa: E731
+    clk12 = phases.get("conv12", {}).get("clock_ghz")
+    if clk12:
+        c2 = np.sum(s12[:, 0, 1:T12 + 1, 1] - s12[:, 0, 1:T12 + 1, 0], axis=1)
+        c1 = np.sum(0.5 * ((s12[:, 1, :T12, 1] - s12[:, 1, :T12, 0]) + (s12[:, 2, :T12, 1] - s12[:, 2, :T12, 0])), axis=1)
+        for name, busy in (("conv1", c1), ("conv2", c2)):
+            bc = float(np.median(busy))
+            row = {"role": "conv12 producer waves 4-7" if name == "conv1" else "conv12 consumer waves 0-3",
+                   "busy_cycles": bc, "mfma_cycles_per_simd": mfma(name), "clock_ghz": clk12,
+                   "mfma_issue_while_busy": mfma(name) / bc, "frac_at_2p4": mfma(name) / bc * clk12 / 2.4,
+                   "bound": "mfma"}
+            if name == "conv1":
+                gbs = bench.BYTES_PER_IMAGE["conv1"] * img_per_wg * g / (bc / (clk12 * 1e9)) / 1e9
+                row.update({"bound": "hbm", "achieved_gbs": gbs, "hbm_frac": gbs / bench.PEAK_HBM_GBS,
+                            "mfma_frac_at_2p4": row["frac_at_2p4"], "frac_at_2p4": gbs / bench.PEAK_HBM_GBS,
+                            "frac_note": "conv1 is HBM-bound (SURVEY §8(d)): frac_at_2p4 here is its algorithmic "
+                                         "bytes (fp32 input + u8 output) per busy time over 8 TB/s"})
+            out[name] = row
+    if hasattr(lib, "qcn_clock_read_ws16"):
+        f = lib.qcn_clock_read_ws16
+        f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+        w = np.zeros((g, 2, 2, 8, 3), np.uint64)
+        _lib.check(f(w.ctypes.data, g), "qcn_clock_read_ws16")
+        w = w.astype(np.float64)
+        for ph, (a, b_, segs) in enumerate((("conv3", "conv4", 1), ("conv5", "conv6", 2))):
+            pn = "conv34" if ph == 0 else "conv56"
+            clk = phases.get(pn, {}).get("clock_ghz")
+            T = int(np.ceil(img_per_wg / segs))
+            if not clk or T + 1 >= 8:
+                continue
+            x = w[:, ph]
+            busy_a = np.sum(x[:, 0, :T, 2] - x[:, 0, :T, 0], axis=1)
+            busy_b = np.sum(x[:, 1, 1:T + 1, 2] - x[:, 1, 1:T + 1, 0], axis=1) + (x[:, 1, T + 1, 0] - x[:, 1, T, 2])
+            for name, busy, role in ((a, busy_a, "A-role waves 0-3"), (b_, busy_b, "B-role waves 4-7")):
+                bc = float(np.median(busy))
+                out[name] = {"role": role, "busy_cycles": bc, "mfma_cycles_per_simd": mfma(name), "clock_ghz": clk,
+                             "mfma_issue_while_busy": mfma(name) / bc, "frac_at_2p4": mfma(name) / bc * clk / 2.4,
+                             "bound": "mfma"}
+    return out
+
+
 def main():
     import bench
     from qconvnet import _lib, data
@@ -173,6 +230,7 @@ def main():
                             "producer_w5_busy": float(np.median(s[:, 2, j, 1] - s[:, 2, j, 0])),
                         }
                     rec["conv12_iterations"] = {"workgroups": int(full.sum()), "tiles": T, "per_iteration": it}
+                    rec["layer_table"] = layer_table(lib, g, img_per_wg, s, T, table, B)
         out["kernels"][n] = rec
     print(json.dumps(out))
     for n, r in out["kernels"].items():

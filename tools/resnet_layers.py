@@ -16,6 +16,7 @@ B = int(os.environ.get("B", 512))
 dev = torch.device("cuda")
 fp = synthetic_resnet(0, device=dev, calib_images=16)
 m = quantize_resnet(fp, [torch.from_numpy(synthetic_images(16, 1))], dev)
+m.fuse_reduce = False   # one "conv" mark per conv layer: the rows below match marks to layers by position
 x = torch.from_numpy(synthetic_images(B, 2)).to(dev)
 for _ in range(3):
     m.run(x)
