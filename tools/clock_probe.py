@@ -66,6 +66,7 @@ def layer_table(lib, g, img_per_wg, s12, T12, phases, B):
     §8(d)): its row also carries its algorithmic bytes per busy time against
     8 TB/s."""
     import bench
+    from qconvnet import _lib
     out = {}
     mfma = lambda n: bench.MAC_PER_IMAGE[n] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)   # noqa: E731
     clk12 = phases.get("conv12", {}).get("clock_ghz")

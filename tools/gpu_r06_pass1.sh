@@ -16,3 +16,5 @@ done
 if [ -f tools/clock/libqconvnet_clock.so ]; then
   timeout -k 10 200 python -u tools/clock_probe.py --batch 1024 > $O/r06_p1_clock.txt 2>&1 || exit 1
 fi
+timeout -k 10 300 python -u tools/w4_ab.py 1024 500 3 > $O/r06_p1_w4_ab.txt 2>&1 || exit 1
+timeout -k 10 300 python -u tools/c16_ab.py 1024 500 3 > $O/r06_p1_c16_ab.txt 2>&1 || exit 1
