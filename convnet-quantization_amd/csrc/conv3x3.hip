@@ -2560,56 +2560,6 @@ QCN_DEV void phase_boundary() {
   __syncthreads();
 }
 
-// Diagnostic builds only (tools/build_variant.sh, -DQCN_GRID_PROBE=F
-// -DQCN_GRID_PROBE_N=K): K grid-wide barriers appended to the one launch, to
-// price in situ what keeping the classifier head inside the persistent launch
-// would cost at its two seams (conv6 -> split-K fc1, split-K partials -> the
-// finisher).  F = 1: one monotonic counter (every workgroup adds 1, target =
-// next multiple of G), relaxed agent-scope polls with s_sleep; F = 2: a
-// two-level tree (groups b % 8 — a label, correctness needs no placement —
-// then the 8 group leaders on a top counter, which publishes a generation).
-// Release fence before the arrival, acquire fence after, lane 0 of wave 0;
-// spins bounded (g_grid_probe_timeout counts give-ups).  Counters are never
-// reset: each barrier's target follows from the arrival ticket.
-#ifdef QCN_GRID_PROBE
-__device__ unsigned g_grid_probe[16 * 32];   // [0]: flat / top, [32 (1 + g)]: group g, [32 * 10]: generation
-__device__ unsigned g_grid_probe_timeout;
-QCN_DEV bool grid_probe_wait(const unsigned* p, unsigned target) {
-  for (int it = 0; it < (1 << 22); ++it) {
-    if ((int)(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-QCN_DEV void grid_probe_barrier(int b, int G) {
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    bool ok;
-    if (QCN_GRID_PROBE == 1) {
-      const unsigned old = __hip_atomic_fetch_add(&g_grid_probe[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = grid_probe_wait(&g_grid_probe[0], (old / (unsigned)G + 1) * (unsigned)G);
-    } else {
-      const int g = b & 7;
-      const unsigned m = (unsigned)((G - g + 7) / 8);
-      const unsigned old = __hip_atomic_fetch_add(&g_grid_probe[32 * (1 + g)], 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned gen = old / m + 1;
-      if (old % m == m - 1) {
-        const unsigned ot = __hip_atomic_fetch_add(&g_grid_probe[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ot % 8 == 7)
-          __hip_atomic_store(&g_grid_probe[32 * 10], ot / 8 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      ok = grid_probe_wait(&g_grid_probe[32 * 10], gen);
-    }
-    if (!ok) __hip_atomic_fetch_add(&g_grid_probe_timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-#endif
-
 // The same launch with the pair phases on the 16x16x64 pipeline (r05).  The
 // conv12 phase is unchanged.  Each pair phase reads only a2 / a4 images its
 // own workgroup wrote (conv3+4 tiles b, b + G, ... of one image each —
@@ -2629,9 +2579,6 @@ void convnet_convs16_kernel(const float* __restrict__ x, int nimg, float in_inv,
   phase_boundary();
   C16_STAMP(2);
   convpair_ws16_body<W16A5, W16B6, EM, EM, KMAJOR, true>(b, G, a4, nimg, z4, w4, e4, z5, w5, e5, a6);
-#ifdef QCN_GRID_PROBE
-  for (int k = 0; k < QCN_GRID_PROBE_N; ++k) grid_probe_barrier(b, G);
-#endif
 #ifdef QCN_CONVNET_STAMP
   __syncthreads();
 #endif

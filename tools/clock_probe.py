@@ -67,7 +67,7 @@ def layer_table(lib, g, img_per_wg, s12, T12, phases, B):
     8 TB/s."""
     import bench
     from qconvnet import _lib
-    out = {}
+    out, periods = {}, {}
     mfma = lambda n: bench.MAC_PER_IMAGE[n] * img_per_wg / (4 * MFMA_MAC_PER_CLK_SIMD)   # noqa: E731
     clk12 = phases.get("conv12", {}).get("clock_ghz")
     if clk12:
@@ -106,7 +106,24 @@ def layer_table(lib, g, img_per_wg, s12, T12, phases, B):
                 out[name] = {"role": role, "busy_cycles": bc, "mfma_cycles_per_simd": mfma(name), "clock_ghz": clk,
                              "mfma_issue_while_busy": mfma(name) / bc, "frac_at_2p4": mfma(name) / bc * clk / 2.4,
                              "bound": "mfma"}
-    return out
+            # the pipeline's periods (median over workgroups, cycles from the
+            # phase's first stamp): A runs tile p, B tile p - 1; period T is B only
+            t0 = np.minimum(x[:, 0, 0, 0], x[:, 1, 0, 0])
+            per = []
+            for p in range(T + 1):
+                row = {"period": p}
+                if p < T:
+                    row.update({"a_start": float(np.median(x[:, 0, p, 0] - t0)),
+                                "a_job": float(np.median(x[:, 0, p, 1] - x[:, 0, p, 0])),
+                                "a_epi_handoff": float(np.median(x[:, 0, p, 2] - x[:, 0, p, 1]))})
+                if p >= 1:
+                    row.update({"b_start": float(np.median(x[:, 1, p, 0] - t0)),
+                                "b_epi": float(np.median(x[:, 1, p, 1] - x[:, 1, p, 0])),
+                                "b_job": float(np.median(x[:, 1, p, 2] - x[:, 1, p, 1]))})
+                per.append(row)
+            per.append({"period": "end", "b_last_epi_done": float(np.median(x[:, 1, T + 1, 0] - t0))})
+            periods[pn] = per
+    return out, periods
 
 
 def main():
@@ -231,7 +248,7 @@ def main():
                             "producer_w5_busy": float(np.median(s[:, 2, j, 1] - s[:, 2, j, 0])),
                         }
                     rec["conv12_iterations"] = {"workgroups": int(full.sum()), "tiles": T, "per_iteration": it}
-                    rec["layer_table"] = layer_table(lib, g, img_per_wg, s, T, table, B)
+                    rec["layer_table"], rec["pair_periods"] = layer_table(lib, g, img_per_wg, s, T, table, B)
         out["kernels"][n] = rec
     print(json.dumps(out))
     for n, r in out["kernels"].items():

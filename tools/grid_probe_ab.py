@@ -5,7 +5,9 @@ forwards, then 500 forwards with HIP-event marks and no host sync between them
 (so no host latency enters the per-launch means).  With --save / --check PATH
 the logits of the last forward are written / compared bit for bit.
 
-    QCN_LIB=... python tools/grid_probe_ab.py NAME [B] [ITERS] [ROUNDS] [--save P | --check P]
+    QCN_LIB=... python tools/grid_probe_ab.py NAME [B] [ITERS] [ROUNDS] [--qdq] [--save P | --check P]
+
+--qdq: the per-layer QDQ net (configs[1]) instead of the static one.
 """
 import os
 import sys
@@ -25,7 +27,8 @@ from qconvnet.qmodel import QuantizedConvNet  # noqa: E402
 
 
 def main():
-    args = [a for a in sys.argv[1:]]
+    args = [a for a in sys.argv[1:] if a != "--qdq"]
+    qdq = "--qdq" in sys.argv[1:]
     save = check = None
     if "--save" in args:
         save = args[args.index("--save") + 1]
@@ -38,7 +41,7 @@ def main():
     iters = int(args[2]) if len(args) > 2 else 1000
     rounds = int(args[3]) if len(args) > 3 else 3
     dev = torch.device("cuda:0")
-    spec, _ = netfix.static_spec(netfix.load(False))
+    spec = netfix.qdq_spec(netfix.load()) if qdq else netfix.static_spec(netfix.load(False))[0]
     model = QuantizedConvNet(spec, dev)
     x = torch.from_numpy(torch_ref.synthetic_images(B, 0)).to(dev)
     t0 = time.perf_counter()
