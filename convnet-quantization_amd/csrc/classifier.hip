@@ -25,9 +25,6 @@
 
 namespace qcn {
 
-#ifndef QCN_FC_U
-#define QCN_FC_U 4           // K chunks per load batch of the split-K loop (build-time)
-#endif
 constexpr int FC_S = 4;      // K split
 constexpr int FC_N1 = 512;   // fc1 features handled by the finisher (64 lanes x 8)
 constexpr int FC_N2 = 16;    // max fc2 outputs
@@ -75,7 +72,7 @@ QCN_DEV void fc_splitk_tile(const uint8_t* __restrict__ x, int m, int k, const i
   const long xs = (long)m * 32, ws = (long)n * 32;   // bytes per K chunk
 
   v16i acc0 = (v16i){0}, acc1 = (v16i){0};
-  constexpr int U = QCN_FC_U;   // chunks per batch; two batches in flight
+  constexpr int U = 4;   // K chunks per load batch of the split-K loop; two batches in flight
   v4i fw[2][U];
   uint4 f0[2][U], f1[2][U];
   auto load = [&](int buf, int c) {

@@ -25,11 +25,6 @@
 #include <cmath>
 #include <type_traits>
 
-// 0: the streaming joins keep the op sequence (diagnostic builds, A/B)
-#ifndef QCN_JOIN_AFF
-#define QCN_JOIN_AFF 1
-#endif
-
 namespace qcn {
 
 // fp32(fp32(acc) + u*v) * mult for two channels (FBGEMM requant before the
@@ -1011,7 +1006,7 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
     // the join in its exact one form (join_affine_solve), whose constants
     // replace s3 / s_r / inv_o in this launch's copy of the arguments
     float j[3];
-    if (QCN_JOIN_AFF && a.z_o == 0 && join_affine_solve(a, j)) {
+    if (a.z_o == 0 && join_affine_solve(a, j)) {
       GemmArgs b = a;
       b.s3 = j[0]; b.s_r = j[1]; b.inv_o = j[2];
       return a.zp_y == 0 ? launch_stream<K, NW, true, P, 0, 2, BL>(b, st) : launch_stream<K, NW, true, P, 1, 2, BL>(b, st);
@@ -1033,7 +1028,7 @@ int stream_modes(GemmArgs& a, hipStream_t st) {
 template <int CR>
 int join_reduce_modes(GemmArgs& a, hipStream_t st) {
   float j[3];
-  if (QCN_JOIN_AFF && a.z_o == 0 && join_affine_solve(a, j)) {
+  if (a.z_o == 0 && join_affine_solve(a, j)) {
     GemmArgs b = a;
     b.s3 = j[0]; b.s_r = j[1]; b.inv_o = j[2];
     return a.zp_y == 0 ? launch_stream<64, 8, true, 4, 0, 2, false, false, CR>(b, st)

@@ -1,4 +1,5 @@
 # Build a diagnostic variant of libqconvnet.so with classifier.hip compiled
+# (r06: the QCN_JOIN_AFF / QCN_FC_U switches this used were removed from csrc/; to rerun, add them back as a patch under tools/patches/.)
 # with extra defines (never the product library):
 #   bash tools/build_variant_fc.sh NAME "-DQCN_FC_U=8"
 set -e

@@ -1,4 +1,5 @@
 # Build a diagnostic variant of libqconvnet.so with convgemm.hip compiled with
+# (r06: the QCN_JOIN_AFF / QCN_FC_U switches this used were removed from csrc/; to rerun, add them back as a patch under tools/patches/.)
 # extra defines (never the product library):
 #   bash tools/build_variant_gemm.sh NAME "-DQCN_JOIN_AFF=0"
 set -e

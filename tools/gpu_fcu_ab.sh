@@ -1,4 +1,5 @@
 # Same-box A/B of the split-K load batch (QCN_FC_U) on the default bench:
+# (r06: the QCN_JOIN_AFF / QCN_FC_U switches this used were removed from csrc/; to rerun, add them back as a patch under tools/patches/.)
 # product (U = 4) vs libqconvnet_fcu8.so / _fcu2.so, two rounds.
 # usage (on the box): bash tools/gpu_fcu_ab.sh TAG
 set -e

@@ -1,4 +1,5 @@
 # One-form residual join check on the box: the ResNet GPU tests, then the
+# (r06: the QCN_JOIN_AFF / QCN_FC_U switches this used were removed from csrc/; to rerun, add them back as a patch under tools/patches/.)
 # ResNet-50 bench (two streams, batch 512) product vs the -DQCN_JOIN_AFF=0
 # variant, two rounds, and the per-layer times of both.
 # usage (on the box): bash tools/gpu_join_check.sh TAG
