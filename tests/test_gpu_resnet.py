@@ -150,10 +150,16 @@ def test_conv_general_oracle(dev, shape, impl):
     (2, 9, 7, 512, 2048, 40, False, 11, True, 0),     # K = 512: activations through the LDS ring
     (3, 28, 28, 512, 128, 0, True, 0, True, None),
     (1, 5, 5, 256, 256, 9, False, 3, False, 9),
+    # K = 1024: the tiled kernel (the r06 K-split streaming form, tools/patches/resnet_k1024_stream.patch, passed these too)
+    (16, 14, 14, 1024, 256, 7, False, 30, True, None),   # the layer-3 reduce, 98 strips
+    (1, 14, 15, 1024, 512, 0, True, 0, False, None),     # ReLU at zy 0 (cvt-only requant), ragged
+    (3, 7, 9, 1024, 128, 131, True, 12, True, None),     # ReLU floor 12 (general clamp), one group
+    (1, 1, 1, 1024, 256, 9, False, 3, True, None),       # one pixel
 ])
 def test_conv1x1_stream_oracle(dev, shape):
     """The streaming 1x1 stride-1 kernel (conv1x1_stream_kernel: K = Cin in
-    {64, 128, 256, 512}, weights and constants in registers, 32-pixel strips) against
+    {64, 128, 256, 512}, weights and constants in registers, 32-pixel strips;
+    the K = 1024 cases run the tiled conv_gemm_kernel) against
     the oracle's conv, and with the fused residual join against conv ->
     add_relu_q."""
     from qconvnet import ops
@@ -236,6 +242,8 @@ def test_conv1x1_join_reduce_oracle(dev, shape):
     (3, 28, 28, 256, 512, 7, 90, True),
     (2, 14, 14, 512, 1024, 0, 0, True),
     (3, 13, 11, 256, 128, 200, 31, False),   # odd input sides, ragged last strip
+    (2, 14, 14, 1024, 2048, 7, 90, True),    # the layer-4 downsample (K = 1024)
+    (3, 13, 11, 1024, 128, 200, 31, False),
 ])
 def test_conv1x1_stride2_stream_oracle(dev, shape):
     """The stride-2 downsample 1x1 on the streaming kernel (rows of the even
