@@ -159,6 +159,7 @@ QCN_DEV EpiK load_epik_lds(const float* ek, int cout, int co_base, int hi) {
 // so the loads overlap the patch staging (visible after the main loop's barriers).
 template <int COUT, int NT>
 QCN_DEV void stage_epik(const ConvEpi& ep, float* ek, int tid) {
+  asm volatile("" : "+v"(tid));   // a fresh copy: no tid-derived offset held across phases
   for (int e = tid; e < 3 * COUT / 4; e += NT) {
     const int arr = e / (COUT / 4), o = (e % (COUT / 4)) * 4;
     const float* src = arr == 0 ? ep.u : (arr == 1 ? ep.v : ep.mult);
@@ -2161,10 +2162,14 @@ QCN_DEV void conv12p_body(int t0, int ts, int T, const float* __restrict__ x, in
     }
     if (!producer) stage_epik<64, 256>(ep1, reinterpret_cast<float*>(lds + L::OFF_EPI1), tid);
     if (!producer) stage_epik<64, 256>(ep2, reinterpret_cast<float*>(lds + L::OFF_EPI2), tid);
-    if (tid < 16)
-      reinterpret_cast<int4*>(lds + L::OFF_CORR2)[tid] = reinterpret_cast<const int4*>(ep2.corr)[tid];
-    if (tid >= 64 && tid < 80)
-      reinterpret_cast<int4*>(lds + L::OFF_CORR1)[tid - 64] = reinterpret_cast<const int4*>(ep1.corr)[tid - 64];
+    {
+      int t = tid;
+      asm volatile("" : "+v"(t));   // a fresh copy: no tid-derived offset held across phases
+      if (t < 16)
+        reinterpret_cast<int4*>(lds + L::OFF_CORR2)[t] = reinterpret_cast<const int4*>(ep2.corr)[t];
+      if (t >= 64 && t < 80)
+        reinterpret_cast<int4*>(lds + L::OFF_CORR1)[t - 64] = reinterpret_cast<const int4*>(ep1.corr)[t - 64];
+    }
     if (wave == 3) {
       // conv1 A operand in the dword-per-tap K order (k' = 4 tap + c, taps
       // 0..7) from the [64][32] (k = 3 tap + c) packing
